@@ -1,0 +1,174 @@
+/*
+ * vmp.h — C ABI of libvmp.so, the MI355X-native batched VM placement/migration
+ * environment (drop-in for the reference's `VmEnv` gym plugin path).
+ *
+ * The reference boundary is a Python gymnasium plugin, not an FFI:
+ *   register("VmEnv-v1", entry_point="vmenv.envs.env:VmEnv")   vmenv/__init__.py:3-6
+ *   env = gym.make("VmEnv-v1", config=Config(**env_cfg))        main.py:47
+ * Every entry point below replaces one method of that class (or of the
+ * FirstFit/BestFit agents) for N independent env instances at once; the
+ * Python layer (vmp/env.py, vmp/batched.py) binds them with ctypes and keeps
+ * the reference's reset()/step()/get_invalid_action_mask() surface.
+ *
+ * Conventions
+ *  - All array pointers passed to a handle created on a GPU are DEVICE
+ *    pointers (e.g. torch.Tensor.data_ptr() on that device); sizes are in
+ *    elements. Layouts are env-major: x[env][...].
+ *  - Every call returns 0 on success or a negative VMP_E* code; the message of
+ *    the last failure on this thread is vmp_last_error().
+ *  - Invalid actions are never errors: they are no-ops reported in `valid`
+ *    (env.py:71-72).
+ *  - A handle is bound to one HIP stream (vmp_set_stream) and is not
+ *    thread-safe; different handles may be used from different threads.
+ */
+#ifndef VMP_H
+#define VMP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VMP_ABI_VERSION 1
+
+#define VMP_OK 0
+#define VMP_EINVAL (-1)
+#define VMP_EDEVICE (-2)
+#define VMP_EOOM (-3)
+#define VMP_ESTATE (-4)
+
+/* reward_function (env.py:123-156) */
+#define VMP_REWARD_WR 0
+#define VMP_REWARD_UT 1
+#define VMP_REWARD_KL 2
+/* sequence (env.py:211-219) */
+#define VMP_SEQ_UNIFORM 0
+#define VMP_SEQ_LOWUNIFORM 1
+#define VMP_SEQ_HIGHUNIFORM 2
+/* heuristic policies (src/agents/firstfit.py:21-38, bestfit.py:21-40) */
+#define VMP_POLICY_FIRSTFIT 0
+#define VMP_POLICY_BESTFIT 1
+
+/* Mirrors vmenv/envs/config.py:4-15 field for field. */
+typedef struct vmp_config {
+  double arrival_rate;      /* Poisson lambda per step */
+  double service_length;    /* Poisson mean; runtime = poisson(L) + 1 */
+  int32_t pms;              /* P */
+  int32_t vms;              /* V (slots) */
+  int64_t training_steps;
+  int64_t eval_steps;
+  int64_t seed;
+  int32_t reward_function;  /* VMP_REWARD_* */
+  int32_t sequence;         /* VMP_SEQ_* */
+  int32_t cap_target_util;  /* bool */
+  int32_t allow_null_action;/* bool: A = P+2 if true else P+1 (env.py:26) */
+  double beta;
+} vmp_config;
+
+/* Per-env counters, vmp_get_counters() row layout (env.py:196-205, 299-318). */
+#define VMP_CTR_TOTAL_REQUESTS 0
+#define VMP_CTR_SERVED 1
+#define VMP_CTR_SUSPEND 2
+#define VMP_CTR_PLACE 3
+#define VMP_CTR_DROPPED 4
+#define VMP_CTR_TIMESTEP 5
+#define VMP_NCTR 6
+/* Per-env float stats, vmp_get_stats() row layout. */
+#define VMP_ST_WAITING_RATIO 0
+#define VMP_ST_TARGET_CPU_MEAN 1
+#define VMP_ST_TARGET_MEM_MEAN 2
+#define VMP_ST_TOTAL_CPU_REQ 3
+#define VMP_ST_TOTAL_MEM_REQ 4
+#define VMP_NST 5
+
+typedef struct vmp_handle vmp_handle;
+
+int vmp_abi_version(void);
+const char *vmp_last_error(void);
+
+/* VmEnv.__init__ (env.py:23-33) for n_env instances on HIP device `device`.
+ * Every env is reset with seeds[i] (host array, n_env entries), i.e.
+ * reset(seed=seeds[i]) -> four numpy PCG64 streams seeded seeds[i]+k
+ * (env.py:172-178). eval_mode starts false (env.py:25). */
+int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32_t device,
+               vmp_handle **out);
+int vmp_destroy(vmp_handle *h);
+int vmp_set_stream(vmp_handle *h, void *hip_stream);
+/* VmEnv.eval (env.py:105-106). */
+int vmp_set_eval(vmp_handle *h, int32_t eval_mode);
+/* Shape helpers: A = action_dim (env.py:26), D = obs dim (env.py:27). */
+int vmp_dims(const vmp_handle *h, int32_t *n_env, int32_t *P, int32_t *V, int32_t *A,
+             int32_t *D);
+
+/* VmEnv.reset (env.py:180-226) for the envs whose env_mask byte is non-zero
+ * (env_mask may be NULL = all). seeds: device int64[n_env] or NULL; a NULL
+ * seeds array is reset(seed=None): streams continue and the VM-size
+ * sequences restart 2*max(training_steps, eval_steps) draws further
+ * (env.py:181-182, 211-219). obs (nullable): device f32[n_env][D]. */
+int vmp_reset(vmp_handle *h, const int64_t *seeds, const uint8_t *env_mask, float *obs);
+
+/* VmEnv.step (env.py:66-103) for every env.
+ *  actions: device int32[n_env][V]
+ *  obs:     device f32[n_env][D]  (nullable)     env.py:295-296
+ *  reward:  device f64[n_env]     (nullable)     env.py:123-156
+ *  done:    device u8[n_env]      (nullable)     env.py:160-163
+ *  valid:   device u8[n_env][V]   (nullable)     env.py:68-72 */
+int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward,
+             uint8_t *done, uint8_t *valid);
+
+/* FirstFitAgent.act / BestFitAgent.act (firstfit.py:21-38, bestfit.py:21-40)
+ * on the current observation of every env -> device int32[n_env][V]. */
+int vmp_heuristic_act(vmp_handle *h, int32_t policy, int32_t *actions);
+
+/* act + step fused in one launch: the action the heuristic takes on the
+ * pre-step observation is applied by step() in the same kernel (the
+ * Base.test loop body, base.py:71-86). actions_out (nullable) receives it. */
+int vmp_heuristic_step(vmp_handle *h, int32_t policy, int32_t *actions_out, float *obs,
+                       double *reward, uint8_t *done, uint8_t *valid);
+
+/* K fused heuristic steps per env in one launch, state resident on chip.
+ * rewards: device f64[k_steps][n_env] (nullable); done_count: device
+ * int64[n_env] (nullable) accumulates the steps whose `terminated` was true. */
+int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double *rewards,
+                          int64_t *done_count);
+
+/* VmEnv.get_invalid_action_mask(masked=True) (env.py:45-53), bit-packed:
+ * device u32[n_env][V][W], W = ceil(A/32); bit a of row v set = invalid. */
+int vmp_mask(vmp_handle *h, uint32_t *bits);
+/* Same mask expanded to the reference's bool layout: device u8[n_env][V][A]. */
+int vmp_mask_bool(vmp_handle *h, uint8_t *mask);
+
+/* Observation of the current state (env.py:295-296): device f32[n_env][D]. */
+int vmp_get_obs(vmp_handle *h, float *obs);
+/* Counters (VMP_CTR_*): device int64[n_env][VMP_NCTR]. */
+int vmp_get_counters(vmp_handle *h, int64_t *counters);
+/* Stats (VMP_ST_*): device f64[n_env][VMP_NST]. */
+int vmp_get_stats(vmp_handle *h, double *stats);
+/* Full reference-dtype state (info / parity): device arrays, each nullable.
+ * placement, remaining: int64[n_env][V]; vm_cpu, vm_mem: f64[n_env][V];
+ * cpu, mem: f64[n_env][P]. */
+int vmp_get_state(vmp_handle *h, int64_t *placement, double *vm_cpu, double *vm_mem,
+                  double *cpu, double *mem, int64_t *remaining);
+/* _get_rank (env.py:320-325) = number of PMs hosting >= 1 VM: int64[n_env]. */
+int vmp_get_rank(vmp_handle *h, int64_t *rank);
+
+/* PPOAgent.update GAE (ppo.py:232-243) over T steps x N envs, reverse scan:
+ *  delta = r + (1-d)*gamma*v' - v;  g = delta + (1-d)*gamma*lambda*g.
+ * All device f32 [T][N] (done as f32 0/1); adv and ret are outputs. */
+int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const float *value,
+            const float *next_value, float gamma, float lam, float *adv, float *ret,
+            void *hip_stream);
+
+/* Masked multi-categorical sampling (ppo.py:115-126): logits f32[B][V*A],
+ * mask bits u32[B][V][W] (nullable = unmasked; masked logits are set to -1e7
+ * as ppo.py:119 does), uniforms for Gumbel-max from (seed, offset).
+ * Outputs: action int32[B][V], logprob f32[B], entropy f32[B]. */
+int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
+                      const uint32_t *mask_bits, uint64_t seed, uint64_t offset,
+                      int32_t *action, float *logprob, float *entropy, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VMP_H */

@@ -1,0 +1,767 @@
+/*
+ * vmp_oracle.c — TEST INFRASTRUCTURE ONLY (the parity checker and the
+ * bench.py cpu_baseline leg). Never linked into, or called by, the product
+ * path in vm-placement-migration-gym_amd/.
+ *
+ * A plain-C restatement of the reference's hot path:
+ *   VmEnv (vmenv/envs/env.py) reset/step/_run_vms/_accept_vm_requests/reward/
+ *   get_invalid_action_mask/_get_obs/_get_rank, and the FirstFit/BestFit agents
+ *   (src/agents/firstfit.py, src/agents/bestfit.py),
+ * plus the third-party arithmetic that path runs through, numpy 1.25.1
+ * (requirements.txt:2; the container has 2.2.6, same streams):
+ *   SeedSequence + PCG64 (numpy/random/bit_generator.pyx, _pcg64.pyx, pcg64.h),
+ *   random_standard_uniform / random_uniform / random_poisson (mult + PTRS) /
+ *   random_loggam (numpy/random/src/distributions/distributions.c),
+ *   np.around (rint(x*100)/100), pairwise add.reduce (loops_utils.h.src),
+ *   np.var/np.mean (numpy/_core/_methods.py), np.argsort's scalar introsort
+ *   aquicksort_/aheapsort_ (npysort/quicksort.cpp, heapsort.cpp).
+ *
+ * Pinned by: tests/golden/traj_*.npz (generated from the unmodified reference by
+ * tools/gen_golden.py), and the published KAT rows of
+ * data/exp_suspension/data.csv (tests/golden/exp_suspension_data.csv).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off -fopenmp, no fast-math).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/vmp.h"
+
+typedef unsigned __int128 u128;
+
+/* ------------------------------------------------------------------ RNG -- */
+#define PCG_MULT ((((u128)0x2360ED051FC65DA4ULL) << 64) | 0x4385DF649FCCF645ULL)
+
+typedef struct {
+  u128 state, inc;
+} pcg64;
+
+/* SeedSequence(seed).generate_state(4, uint64) (bit_generator.pyx, mix_entropy
+ * and generate_state), for non-negative integer seeds < 2**64. */
+static void seedseq_words(uint64_t seed, uint64_t out[4]) {
+  const uint32_t INIT_A = 0x43b0d7e5u, MULT_A = 0x931e8875u, INIT_B = 0x8b51f9ddu,
+                 MULT_B = 0x58f38dedu, MIX_L = 0xca01f9ddu, MIX_R = 0x4973f715u;
+  uint32_t ent[2];
+  int n_ent = 1;
+  ent[0] = (uint32_t)seed;
+  if (seed >> 32) {
+    ent[1] = (uint32_t)(seed >> 32);
+    n_ent = 2;
+  }
+  uint32_t pool[4];
+  uint32_t hc = INIT_A;
+#define HASHMIX(v, out_)           \
+  do {                             \
+    uint32_t _v = (v);             \
+    _v ^= hc;                      \
+    hc *= MULT_A;                  \
+    _v *= hc;                      \
+    _v ^= _v >> 16;                \
+    (out_) = _v;                   \
+  } while (0)
+  for (int i = 0; i < 4; i++) HASHMIX(i < n_ent ? ent[i] : 0u, pool[i]);
+  for (int s = 0; s < 4; s++)
+    for (int d = 0; d < 4; d++)
+      if (s != d) {
+        uint32_t h;
+        HASHMIX(pool[s], h);
+        uint32_t r = MIX_L * pool[d] - MIX_R * h;
+        r ^= r >> 16;
+        pool[d] = r;
+      }
+#undef HASHMIX
+  uint32_t w[8];
+  uint32_t hb = INIT_B;
+  for (int i = 0; i < 8; i++) {
+    uint32_t d = pool[i & 3];
+    d ^= hb;
+    hb *= MULT_B;
+    d *= hb;
+    d ^= d >> 16;
+    w[i] = d;
+  }
+  for (int i = 0; i < 4; i++) out[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+}
+
+/* pcg64_set_seed -> pcg_setseq_128_srandom_r (pcg64.h). */
+static void pcg_seed(pcg64 *r, uint64_t seed) {
+  uint64_t v[4];
+  seedseq_words(seed, v);
+  u128 s = ((u128)v[0] << 64) | v[1];
+  u128 i = ((u128)v[2] << 64) | v[3];
+  r->state = 0;
+  r->inc = (i << 1) | 1;
+  r->state = r->state * PCG_MULT + r->inc;
+  r->state += s;
+  r->state = r->state * PCG_MULT + r->inc;
+}
+
+static inline uint64_t pcg_next64(pcg64 *r) {
+  r->state = r->state * PCG_MULT + r->inc;
+  uint64_t hi = (uint64_t)(r->state >> 64), lo = (uint64_t)r->state;
+  unsigned rot = (unsigned)(r->state >> 122);
+  uint64_t x = hi ^ lo;
+  return (x >> rot) | (x << ((64 - rot) & 63));
+}
+
+/* pcg_advance_lcg_128 (pcg64.c): jump the LCG by delta steps. */
+static void pcg_advance(pcg64 *r, u128 delta) {
+  u128 cur_mult = PCG_MULT, cur_plus = r->inc, acc_mult = 1, acc_plus = 0;
+  while (delta > 0) {
+    if (delta & 1) {
+      acc_mult *= cur_mult;
+      acc_plus = acc_plus * cur_mult + cur_plus;
+    }
+    cur_plus = (cur_mult + 1) * cur_plus;
+    cur_mult *= cur_mult;
+    delta >>= 1;
+  }
+  r->state = acc_mult * r->state + acc_plus;
+}
+
+static inline double next_double(pcg64 *r) {
+  return (double)(pcg_next64(r) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+/* random_loggam (distributions.c). */
+static double loggam(double x) {
+  static const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03,
+                               7.936507936507937e-04, -5.952380952380952e-04,
+                               8.417508417508418e-04, -1.917526917526918e-03,
+                               6.410256410256410e-03, -2.955065359477124e-02,
+                               1.796443723688307e-01, -1.39243221690590e+00};
+  int64_t n;
+  if (x == 1.0 || x == 2.0) return 0.0;
+  n = (x < 7.0) ? (int64_t)(7 - x) : 0;
+  double x0 = x + n;
+  double x2 = (1.0 / x0) * (1.0 / x0);
+  const double lg2pi = 1.8378770664093453e+00;
+  double gl0 = a[9];
+  for (int k = 8; k >= 0; k--) {
+    gl0 *= x2;
+    gl0 += a[k];
+  }
+  double gl = gl0 / x0 + 0.5 * lg2pi + (x0 - 0.5) * log(x0) - x0;
+  if (x < 7.0) {
+    for (int64_t k = 1; k <= n; k++) {
+      gl -= log(x0 - 1.0);
+      x0 -= 1.0;
+    }
+  }
+  return gl;
+}
+
+/* random_poisson (distributions.c): mult method below 10, PTRS at >= 10. */
+static int64_t poisson(pcg64 *r, double lam) {
+  if (lam >= 10) {
+    double slam = sqrt(lam), loglam = log(lam);
+    double b = 0.931 + 2.53 * slam;
+    double a = -0.059 + 0.02483 * b;
+    double invalpha = 1.1239 + 1.1328 / (b - 3.4);
+    double vr = 0.9277 - 3.6224 / (b - 2);
+    for (;;) {
+      double U = next_double(r) - 0.5;
+      double V = next_double(r);
+      double us = 0.5 - fabs(U);
+      int64_t k = (int64_t)floor((2 * a / us + b) * U + lam + 0.43);
+      if ((us >= 0.07) && (V <= vr)) return k;
+      if ((k < 0) || ((us < 0.013) && (V > us))) continue;
+      if ((log(V) + log(invalpha) - log(a / (us * us) + b)) <=
+          (-lam + k * loglam - loggam(k + 1)))
+        return k;
+    }
+  } else if (lam == 0) {
+    return 0;
+  } else {
+    double enlam = exp(-lam), prod = 1.0;
+    int64_t X = 0;
+    for (;;) {
+      prod *= next_double(r);
+      if (prod > enlam)
+        X += 1;
+      else
+        return X;
+    }
+  }
+}
+
+/* ------------------------------------------------------- numpy reductions -- */
+/* DOUBLE_pairwise_sum (numpy/_core/src/umath/loops_utils.h.src), PW_BLOCKSIZE 128.
+ * add.reduce initialises with the identity 0.0 and adds this result once. */
+static double pw_sum(const double *a, int64_t n) {
+  if (n < 8) {
+    double res = 0.;
+    for (int64_t i = 0; i < n; i++) res += a[i];
+    return res;
+  } else if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; j++) r[j] = a[j];
+    int64_t i;
+    for (i = 8; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; j++) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; i++) res += a[i];
+    return res;
+  } else {
+    int64_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_sum(a, n2) + pw_sum(a + n2, n - n2);
+  }
+}
+static double np_sum(const double *a, int64_t n) { return 0.0 + pw_sum(a, n); }
+static double np_mean(const double *a, int64_t n) { return np_sum(a, n) / (double)n; }
+/* _methods._var with ddof=0: mean, (x-mean)**2 elementwise, sum, / n. */
+static double np_var(const double *a, int64_t n, double *tmp) {
+  double m = np_sum(a, n) / (double)n;
+  for (int64_t i = 0; i < n; i++) {
+    double d = a[i] - m;
+    tmp[i] = d * d;
+  }
+  return np_sum(tmp, n) / (double)n;
+}
+
+/* ------------------------------------------------ numpy scalar argsort -- */
+/* Tag::less for floats: a < b || (b != b && a == a). */
+static inline int fless(float a, float b) { return a < b || (b != b && a == a); }
+
+static void aheapsort_f32(const float *v, int64_t *tosort, int64_t n) {
+  int64_t *a = tosort - 1, i, j, l, tmp;
+  for (l = n >> 1; l > 0; --l) {
+    tmp = a[l];
+    for (i = l, j = l << 1; j <= n;) {
+      if (j < n && fless(v[a[j]], v[a[j + 1]])) j += 1;
+      if (fless(v[tmp], v[a[j]])) {
+        a[i] = a[j];
+        i = j;
+        j += j;
+      } else
+        break;
+    }
+    a[i] = tmp;
+  }
+  for (; n > 1;) {
+    tmp = a[n];
+    a[n] = a[1];
+    n -= 1;
+    for (i = 1, j = 2; j <= n;) {
+      if (j < n && fless(v[a[j]], v[a[j + 1]])) j++;
+      if (fless(v[tmp], v[a[j]])) {
+        a[i] = a[j];
+        i = j;
+        j += j;
+      } else
+        break;
+    }
+    a[i] = tmp;
+  }
+}
+
+#define ISWAP(a, b)  \
+  do {               \
+    int64_t _t = (a); \
+    (a) = (b);       \
+    (b) = _t;        \
+  } while (0)
+
+/* aquicksort_<npy::float_tag> (npysort/quicksort.cpp), tosort = arange(num). */
+static void aquicksort_f32(const float *v, int64_t *tosort, int64_t num) {
+  float vp;
+  int64_t *pl = tosort, *pr = tosort + num - 1;
+  int64_t *stack[128], **sptr = stack, *pm, *pi, *pj, *pk, vi;
+  int depth[128], *psdepth = depth;
+  int cdepth = 0;
+  for (int64_t u = num; u >>= 1;) cdepth++;
+  cdepth *= 2;
+  for (;;) {
+    if (cdepth < 0) {
+      aheapsort_f32(v, pl, pr - pl + 1);
+      goto stack_pop;
+    }
+    while ((pr - pl) > 15) {
+      pm = pl + ((pr - pl) >> 1);
+      if (fless(v[*pm], v[*pl])) ISWAP(*pm, *pl);
+      if (fless(v[*pr], v[*pm])) ISWAP(*pr, *pm);
+      if (fless(v[*pm], v[*pl])) ISWAP(*pm, *pl);
+      vp = v[*pm];
+      pi = pl;
+      pj = pr - 1;
+      ISWAP(*pm, *pj);
+      for (;;) {
+        do ++pi;
+        while (fless(v[*pi], vp));
+        do --pj;
+        while (fless(vp, v[*pj]));
+        if (pi >= pj) break;
+        ISWAP(*pi, *pj);
+      }
+      pk = pr - 1;
+      ISWAP(*pi, *pk);
+      if (pi - pl < pr - pi) {
+        *sptr++ = pi + 1;
+        *sptr++ = pr;
+        pr = pi - 1;
+      } else {
+        *sptr++ = pl;
+        *sptr++ = pi - 1;
+        pl = pi + 1;
+      }
+      *psdepth++ = --cdepth;
+    }
+    for (pi = pl + 1; pi <= pr; ++pi) {
+      vi = *pi;
+      vp = v[vi];
+      pj = pi;
+      pk = pi - 1;
+      while (pj > pl && fless(vp, v[*pk])) *pj-- = *pk--;
+      *pj = vi;
+    }
+  stack_pop:
+    if (sptr == stack) break;
+    pr = *(--sptr);
+    pl = *(--sptr);
+    cdepth = *(--psdepth);
+  }
+}
+
+/* ------------------------------------------------------------- the env -- */
+typedef struct oenv {
+  vmp_config cfg;
+  int eval_mode;
+  int P, V, A, WAIT, NUL, D;
+  int64_t M2; /* 2*max(training_steps, eval_steps): sequence length (env.py:210) */
+  int64_t *placement, *remaining;
+  double *vm_cpu, *vm_mem, *cpu, *mem;
+  int64_t timestep, total_requests, served, suspend_action, place_action, dropped;
+  double total_cpu_req, total_mem_req, waiting_ratio, tcm, tmm;
+  pcg64 rng[4];
+  pcg64 seq_base[2]; /* rng1/rng2 state at the last reset: sequence element 0 */
+  double *tmp, *tmp2, *tmp3;
+  int64_t *acc;
+  float *f_cpu, *f_mem, *f_vcpu, *f_vmem, *f_key;
+  int64_t *order;
+} oenv;
+
+static double seq_lo(int s) { return s == VMP_SEQ_HIGHUNIFORM ? 0.25 : 0.1; }
+static double seq_hi(int s) { return s == VMP_SEQ_LOWUNIFORM ? 0.65 : 1.0; }
+
+void oracle_destroy(oenv *e) {
+  if (!e) return;
+  free(e->placement);
+  free(e->remaining);
+  free(e->vm_cpu);
+  free(e->vm_mem);
+  free(e->cpu);
+  free(e->mem);
+  free(e->tmp);
+  free(e->tmp2);
+  free(e->tmp3);
+  free(e->acc);
+  free(e->f_cpu);
+  free(e->f_mem);
+  free(e->f_vcpu);
+  free(e->f_vmem);
+  free(e->f_key);
+  free(e->order);
+  free(e);
+}
+
+/* VmEnv.reset (env.py:180-226). has_seed=0 is reset(seed=None). */
+void oracle_reset(oenv *e, int has_seed, int64_t seed) {
+  int V = e->V, P = e->P;
+  if (has_seed) {
+    for (int k = 0; k < 4; k++) pcg_seed(&e->rng[k], (uint64_t)(seed + k)); /* seed() 172-178 */
+  } else {
+    /* streams continue; rng1/rng2 sit after the previous 2M-draw sequences */
+    for (int k = 0; k < 2; k++) {
+      e->rng[k] = e->seq_base[k];
+      pcg_advance(&e->rng[k], (u128)e->M2);
+    }
+  }
+  e->seq_base[0] = e->rng[0];
+  e->seq_base[1] = e->rng[1];
+  for (int v = 0; v < V; v++) {
+    e->placement[v] = e->NUL;
+    e->remaining[v] = 0;
+    e->vm_cpu[v] = e->vm_mem[v] = 0.0;
+  }
+  for (int p = 0; p < P; p++) e->cpu[p] = e->mem[p] = 0.0;
+  e->timestep = 1;
+  e->total_requests = e->served = e->suspend_action = e->place_action = e->dropped = 0;
+  e->total_cpu_req = e->total_mem_req = 0.0;
+  e->waiting_ratio = e->tcm = e->tmm = 0.0;
+}
+
+oenv *oracle_create(const vmp_config *cfg) {
+  oenv *e = (oenv *)calloc(1, sizeof(oenv));
+  e->cfg = *cfg;
+  e->P = cfg->pms;
+  e->V = cfg->vms;
+  e->A = cfg->allow_null_action ? cfg->pms + 2 : cfg->pms + 1;
+  e->WAIT = cfg->pms;
+  e->NUL = cfg->pms + 1;
+  e->D = 3 * cfg->vms + 2 * cfg->pms;
+  int64_t M = cfg->training_steps > cfg->eval_steps ? cfg->training_steps : cfg->eval_steps;
+  e->M2 = 2 * M;
+  int V = e->V, P = e->P, n = V > P ? V : P;
+  e->placement = (int64_t *)malloc(sizeof(int64_t) * V);
+  e->remaining = (int64_t *)malloc(sizeof(int64_t) * V);
+  e->vm_cpu = (double *)malloc(sizeof(double) * V);
+  e->vm_mem = (double *)malloc(sizeof(double) * V);
+  e->cpu = (double *)malloc(sizeof(double) * P);
+  e->mem = (double *)malloc(sizeof(double) * P);
+  e->tmp = (double *)malloc(sizeof(double) * (n + 8));
+  e->tmp2 = (double *)malloc(sizeof(double) * (n + 8));
+  e->tmp3 = (double *)malloc(sizeof(double) * (n + 8));
+  e->acc = (int64_t *)malloc(sizeof(int64_t) * (V + 1));
+  e->f_cpu = (float *)malloc(sizeof(float) * P);
+  e->f_mem = (float *)malloc(sizeof(float) * P);
+  e->f_key = (float *)malloc(sizeof(float) * P);
+  e->f_vcpu = (float *)malloc(sizeof(float) * V);
+  e->f_vmem = (float *)malloc(sizeof(float) * V);
+  e->order = (int64_t *)malloc(sizeof(int64_t) * P);
+  oracle_reset(e, 1, cfg->seed);
+  return e;
+}
+
+void oracle_set_eval(oenv *e, int mode) { e->eval_mode = mode; }
+
+/* validate + _resource_valid (env.py:35-42, 55-56). */
+static inline int valid_move(const oenv *e, int v, int64_t c, int64_t t) {
+  if (c == t) return 1;
+  if (c == e->WAIT)
+    return t >= 0 && t < e->WAIT && e->cpu[t] + e->vm_cpu[v] <= 1 && e->mem[t] + e->vm_mem[v] <= 1;
+  if (c < e->WAIT) return t == e->WAIT;
+  return 0;
+}
+
+/* _run_vms (env.py:244-268). */
+static void run_vms(oenv *e) {
+  int64_t n_term = 0;
+  for (int v = 0; v < e->V; v++) {
+    if (e->placement[v] < e->WAIT && e->remaining[v] > 0) e->remaining[v] -= 1;
+  }
+  for (int v = 0; v < e->V; v++) {
+    int64_t pm = e->placement[v];
+    if (pm < e->WAIT && e->remaining[v] == 0) {
+      e->cpu[pm] -= e->vm_cpu[v];
+      e->mem[pm] -= e->vm_mem[v];
+      e->placement[v] = e->NUL;
+      e->vm_cpu[v] = e->vm_mem[v] = 0.0;
+      e->remaining[v] = 0;
+      n_term++;
+    }
+  }
+  e->served += n_term;
+  for (int p = 0; p < e->P; p++) {
+    if (e->cpu[p] < 1e-7) e->cpu[p] = 0;
+    if (e->mem[p] < 1e-7) e->mem[p] = 0;
+  }
+}
+
+/* _accept_vm_requests (env.py:271-293). */
+static void accept_vm_requests(oenv *e) {
+  int64_t arrivals = poisson(&e->rng[2], e->cfg.arrival_rate);
+  e->total_requests += arrivals;
+  int64_t n_null = 0;
+  for (int v = 0; v < e->V; v++) n_null += (e->placement[v] == e->NUL);
+  int64_t k = arrivals < n_null ? arrivals : n_null;
+  double lo = seq_lo(e->cfg.sequence), rng_w = seq_hi(e->cfg.sequence) - lo;
+  int64_t j = 0;
+  for (int v = 0; v < e->V && j < k; v++) {
+    if (e->placement[v] != e->NUL) continue;
+    e->placement[v] = e->WAIT;
+    /* np.around(rng.uniform(lo, hi), 2): rint(x*100)/100 */
+    e->vm_cpu[v] = rint((lo + rng_w * next_double(&e->rng[0])) * 100.0) / 100.0;
+    e->vm_mem[v] = rint((lo + rng_w * next_double(&e->rng[1])) * 100.0) / 100.0;
+    e->tmp[j] = e->vm_cpu[v];
+    e->tmp2[j] = e->vm_mem[v];
+    e->acc[j] = v;
+    j++;
+  }
+  e->total_cpu_req += np_sum(e->tmp, k);
+  e->total_mem_req += np_sum(e->tmp2, k);
+  /* planned = rng4.poisson(L, size=k) + 1 in ascending slot order; no draw if k == 0 */
+  for (j = 0; j < k; j++) e->remaining[e->acc[j]] = poisson(&e->rng[3], e->cfg.service_length) + 1;
+  e->dropped += arrivals - k;
+}
+
+/* kl_divergence (env.py:8-17) with numpy/LAPACK/OpenBLAS evaluation order. */
+static double kl_reward(double tcm, double tmm, double tcv, double tmv, double cm, double mm,
+                        double cv, double mv) {
+  double det_q = exp((0.0 + log(cv)) + log(mv));
+  double det_p = exp((0.0 + log(tcv)) + log(tmv));
+  double qi0 = 1.0 / cv, qi1 = 1.0 / mv;
+  double tr = qi0 * tcv + qi1 * tmv;
+  double d0 = tcm - cm, d1 = tmm - mm;
+  double m1 = fma(d1 * qi1, d1, (d0 * qi0) * d0);
+  double kl = 0.5 * ((((log(det_q / det_p) - 2) + tr) + m1) - tr);
+  return -kl;
+}
+
+/* _process_action stats + reward (env.py:112-156). */
+static double stats_reward(oenv *e) {
+  int64_t n_ex = 0, n_w = 0;
+  for (int v = 0; v < e->V; v++) {
+    if (e->placement[v] <= e->WAIT) {
+      e->tmp[n_ex] = e->vm_cpu[v];
+      e->tmp2[n_ex] = e->vm_mem[v];
+      n_ex++;
+    }
+    n_w += (e->placement[v] == e->WAIT);
+  }
+  e->waiting_ratio = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
+  e->tcm = np_sum(e->tmp, n_ex) / (double)e->P;
+  if (e->cfg.cap_target_util && e->tcm > 1) e->tcm = 1.0;
+  e->tmm = np_sum(e->tmp2, n_ex) / (double)e->P;
+  if (e->cfg.cap_target_util && e->tmm > 1) e->tmm = 1.0;
+  if (n_ex == 0) return 0.0;
+  switch (e->cfg.reward_function) {
+    case VMP_REWARD_KL: {
+      double *scratch = e->tmp3;
+      double cm = np_mean(e->cpu, e->P), mm = np_mean(e->mem, e->P);
+      double cv = np_var(e->cpu, e->P, scratch), mv = np_var(e->mem, e->P, scratch);
+      if (cv == 0) cv = 1e-6;
+      if (mv == 0) mv = 1e-6;
+      double tcv = np_var(e->tmp, n_ex, scratch), tmv = np_var(e->tmp2, n_ex, scratch);
+      if (tcv == 0) tcv = 1e-6;
+      if (tmv == 0) tmv = 1e-6;
+      if (e->tcm == 0 || e->tmm == 0) return 0.0;
+      return kl_reward(e->tcm, e->tmm, tcv, tmv, cm, mm, cv, mv);
+    }
+    case VMP_REWARD_UT:
+      return e->cfg.beta * np_sum(e->cpu, e->P) + (1 - e->cfg.beta) * np_sum(e->mem, e->P);
+    default:
+      return -e->waiting_ratio;
+  }
+}
+
+/* VmEnv.step (env.py:66-103). action: int64[V]; valid (nullable): u8[V]. */
+void oracle_step(oenv *e, const int64_t *action, uint8_t *valid, double *reward, int *terminated) {
+  for (int v = 0; v < e->V; v++) {
+    int64_t c = e->placement[v], t = action[v];
+    int ok = valid_move(e, v, c, t);
+    if (valid) valid[v] = (uint8_t)ok;
+    if (!ok) continue;
+    e->placement[v] = t;
+    if (t == c) {
+    } else if (t == e->WAIT) {
+      e->cpu[c] -= e->vm_cpu[v];
+      e->mem[c] -= e->vm_mem[v];
+      e->suspend_action++;
+    } else if (t < e->WAIT) {
+      e->cpu[t] += e->vm_cpu[v];
+      e->mem[t] += e->vm_mem[v];
+      e->place_action++;
+    }
+  }
+  run_vms(e);
+  accept_vm_requests(e);
+  double r = stats_reward(e);
+  int64_t lim = e->eval_mode ? e->cfg.eval_steps : e->cfg.training_steps;
+  *terminated = e->timestep >= lim;
+  if (reward) *reward = r;
+  e->timestep += 1;
+}
+
+/* _get_obs (env.py:295-296). */
+void oracle_obs(const oenv *e, float *obs) {
+  int V = e->V, P = e->P;
+  for (int v = 0; v < V; v++) {
+    obs[v] = (float)e->placement[v];
+    obs[V + v] = (float)e->vm_cpu[v];
+    obs[2 * V + v] = (float)e->vm_mem[v];
+  }
+  for (int p = 0; p < P; p++) {
+    obs[3 * V + p] = (float)e->cpu[p];
+    obs[3 * V + P + p] = (float)e->mem[p];
+  }
+}
+
+/* get_invalid_action_mask(masked=True) (env.py:45-53): u8[V][A], 1 = invalid. */
+void oracle_mask(const oenv *e, uint8_t *mask) {
+  for (int v = 0; v < e->V; v++)
+    for (int a = 0; a < e->A; a++)
+      mask[(int64_t)v * e->A + a] = (uint8_t)!valid_move(e, v, e->placement[v], a);
+}
+
+static void load_f32_obs(oenv *e) {
+  for (int p = 0; p < e->P; p++) {
+    e->f_cpu[p] = (float)e->cpu[p];
+    e->f_mem[p] = (float)e->mem[p];
+  }
+  for (int v = 0; v < e->V; v++) {
+    e->f_vcpu[v] = (float)e->vm_cpu[v];
+    e->f_vmem[v] = (float)e->vm_mem[v];
+  }
+}
+
+/* FirstFitAgent.act (firstfit.py:21-38): float32 on the observation; the
+ * local memory copy is NOT updated after a tentative placement (line 36). */
+void oracle_firstfit(oenv *e, int64_t *action) {
+  load_f32_obs(e);
+  for (int v = 0; v < e->V; v++) {
+    action[v] = e->placement[v];
+    if (e->placement[v] != e->WAIT) continue;
+    for (int p = 0; p < e->P; p++) {
+      float c = e->f_cpu[p] + e->f_vcpu[v];
+      float m = e->f_mem[p] + e->f_vmem[v];
+      if (c <= 1.0f && m <= 1.0f) {
+        action[v] = p;
+        e->f_cpu[p] += e->f_vcpu[v];
+        break;
+      }
+    }
+  }
+}
+
+/* BestFitAgent.act (bestfit.py:21-40): PMs visited in
+ * np.flip(np.argsort(cpu + memory)) (scalar introsort), cpu and memory both
+ * updated. The order is re-sorted for every waiting VM as the reference
+ * does (line 33); it only changes after a successful placement. */
+void oracle_bestfit(oenv *e, int64_t *action) {
+  load_f32_obs(e);
+  int P = e->P, dirty = 1;
+  for (int v = 0; v < e->V; v++) {
+    action[v] = e->placement[v];
+    if (e->placement[v] != e->WAIT) continue;
+    if (dirty) {
+      for (int p = 0; p < P; p++) {
+        e->f_key[p] = e->f_cpu[p] + e->f_mem[p];
+        e->order[p] = p;
+      }
+      aquicksort_f32(e->f_key, e->order, P);
+      dirty = 0;
+    }
+    for (int i = P - 1; i >= 0; i--) {
+      int64_t p = e->order[i];
+      float c = e->f_cpu[p] + e->f_vcpu[v];
+      float m = e->f_mem[p] + e->f_vmem[v];
+      if (c <= 1.0f && m <= 1.0f) {
+        action[v] = p;
+        e->f_cpu[p] += e->f_vcpu[v];
+        e->f_mem[p] += e->f_vmem[v];
+        dirty = 1;
+        break;
+      }
+    }
+  }
+}
+
+/* _get_rank (env.py:320-325): rank of a one-hot V x P matrix whose column
+ * supports are disjoint = number of distinct PMs hosting a VM. */
+int64_t oracle_rank(const oenv *e) {
+  int64_t r = 0;
+  uint8_t *used = (uint8_t *)calloc(e->P, 1);
+  for (int v = 0; v < e->V; v++)
+    if (e->placement[v] < e->WAIT && !used[e->placement[v]]) {
+      used[e->placement[v]] = 1;
+      r++;
+    }
+  free(used);
+  return r;
+}
+
+/* Accessors for tests. */
+void oracle_get_state(const oenv *e, int64_t *placement, double *vm_cpu, double *vm_mem,
+                      double *cpu, double *mem, int64_t *remaining) {
+  memcpy(placement, e->placement, sizeof(int64_t) * e->V);
+  memcpy(vm_cpu, e->vm_cpu, sizeof(double) * e->V);
+  memcpy(vm_mem, e->vm_mem, sizeof(double) * e->V);
+  memcpy(cpu, e->cpu, sizeof(double) * e->P);
+  memcpy(mem, e->mem, sizeof(double) * e->P);
+  memcpy(remaining, e->remaining, sizeof(int64_t) * e->V);
+}
+void oracle_get_counters(const oenv *e, int64_t *c, double *st) {
+  c[0] = e->total_requests;
+  c[1] = e->served;
+  c[2] = e->suspend_action;
+  c[3] = e->place_action;
+  c[4] = e->dropped;
+  c[5] = e->timestep;
+  st[0] = e->waiting_ratio;
+  st[1] = e->tcm;
+  st[2] = e->tmm;
+  st[3] = e->total_cpu_req;
+  st[4] = e->total_mem_req;
+}
+
+/* -------------------------------------------------------- RNG test hooks -- */
+void oracle_pcg_seed(uint64_t seed, uint64_t out[4]) {
+  pcg64 r;
+  pcg_seed(&r, seed);
+  out[0] = (uint64_t)(r.state >> 64);
+  out[1] = (uint64_t)r.state;
+  out[2] = (uint64_t)(r.inc >> 64);
+  out[3] = (uint64_t)r.inc;
+}
+void oracle_pcg_raw(uint64_t seed, int64_t n, uint64_t *out) {
+  pcg64 r;
+  pcg_seed(&r, seed);
+  for (int64_t i = 0; i < n; i++) out[i] = pcg_next64(&r);
+}
+void oracle_pcg_double(uint64_t seed, int64_t n, double *out) {
+  pcg64 r;
+  pcg_seed(&r, seed);
+  for (int64_t i = 0; i < n; i++) out[i] = next_double(&r);
+}
+void oracle_pcg_around(uint64_t seed, int64_t n, double lo, double hi, double *out) {
+  pcg64 r;
+  pcg_seed(&r, seed);
+  for (int64_t i = 0; i < n; i++) out[i] = rint((lo + (hi - lo) * next_double(&r)) * 100.0) / 100.0;
+}
+/* n poisson draws, then the next raw u64 (stream-position check). */
+uint64_t oracle_pcg_poisson(uint64_t seed, double lam, int64_t n, int64_t *out) {
+  pcg64 r;
+  pcg_seed(&r, seed);
+  for (int64_t i = 0; i < n; i++) out[i] = poisson(&r, lam);
+  return pcg_next64(&r);
+}
+uint64_t oracle_pcg_advance_raw(uint64_t seed, uint64_t delta) {
+  pcg64 r;
+  pcg_seed(&r, seed);
+  pcg_advance(&r, delta);
+  return pcg_next64(&r);
+}
+double oracle_pw_sum(const double *a, int64_t n) { return np_sum(a, n); }
+void oracle_argsort_f32(const float *v, int64_t n, int64_t *out) {
+  for (int64_t i = 0; i < n; i++) out[i] = i;
+  aquicksort_f32(v, out, n);
+}
+
+/* ------------------------------------------------ batched CPU baseline -- */
+/* n_env independent envs (seeds seed0 + stride*i), `steps` heuristic act+step
+ * iterations each (the Base.test loop body, base.py:71-86), OpenMP over envs.
+ * Outputs per env: reward sum and counters (VMP_NCTR). Returns env-steps done. */
+int64_t oracle_rollout(const vmp_config *cfg, int32_t n_env, int64_t seed0, int64_t stride,
+                       int64_t steps, int32_t policy, int32_t eval_mode, int32_t n_threads,
+                       double *reward_sum, int64_t *counters) {
+#pragma omp parallel for schedule(dynamic, 1) num_threads(n_threads)
+  for (int32_t i = 0; i < n_env; i++) {
+    vmp_config c = *cfg;
+    c.seed = seed0 + stride * (int64_t)i;
+    oenv *e = oracle_create(&c);
+    oracle_set_eval(e, eval_mode);
+    int64_t *act = (int64_t *)malloc(sizeof(int64_t) * e->V);
+    double rs = 0.0;
+    for (int64_t s = 0; s < steps; s++) {
+      if (policy == VMP_POLICY_BESTFIT)
+        oracle_bestfit(e, act);
+      else
+        oracle_firstfit(e, act);
+      double r;
+      int term;
+      oracle_step(e, act, NULL, &r, &term);
+      rs += r;
+    }
+    if (reward_sum) reward_sum[i] = rs;
+    if (counters) {
+      double st[VMP_NST];
+      oracle_get_counters(e, counters + (int64_t)i * VMP_NCTR, st);
+    }
+    free(act);
+    oracle_destroy(e);
+  }
+  return (int64_t)n_env * steps;
+}
