@@ -163,7 +163,8 @@ int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const 
 /* Masked multi-categorical sampling (ppo.py:115-126): logits f32[B][V*A],
  * mask bits u32[B][V][W] (nullable = unmasked; masked logits are set to -1e7
  * as ppo.py:119 does), uniforms for Gumbel-max from (seed, offset).
- * Outputs: action int32[B][V], logprob f32[B], entropy f32[B]. */
+ * Outputs per (sample, VM) row: action int32[B][V], logprob f32[B][V],
+ * entropy f32[B][V] (the caller sums over V as ppo.py:124-125 does). */
 int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
                       const uint32_t *mask_bits, uint64_t seed, uint64_t offset,
                       int32_t *action, float *logprob, float *entropy, void *hip_stream);

@@ -1,0 +1,228 @@
+"""HIP path parity (MI355X): libvmp.so through the C ABI against the golden
+reference fixtures and the C oracle. Integer state/counters must be bit-exact;
+wr/ut rewards bit-exact; kl within 1e-12 relative (device log/exp vs glibc)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests import traj as T
+from tests.golden_hash import obs_hash, state_hash
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _cfg(d, **over):
+    from vmp.config import Config
+    c = dict(d)
+    c.update(over)
+    return Config(**c)
+
+
+def _np_state(b, i=0):
+    return {k: v[i].cpu().numpy() for k, v in b.state().items()}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+
+
+@pytest.mark.parametrize("name", T.traj_names())
+def test_trajectory_replay_hip(name):
+    from vmp.batched import BatchedVmEnv
+    d = T.load(name)
+    envs = []
+    for r in d["rewards"]:
+        b = BatchedVmEnv(_cfg(d["config"], reward_function=r), 1, seeds=[d["config"]["seed"]],
+                         device=DEV)
+        b.eval(bool(d["eval_mode"]))
+        envs.append(b)
+    acts = T.sparse_actions(d)
+    masks = {int(t): i for i, t in enumerate(d["mask_at"])}
+    V = d["config"]["vms"]
+    for t in range(d["T"]):
+        if t == d["reset_none_at"]:
+            for b in envs:
+                b.reset(None)
+        b0 = envs[0]
+        if t in masks:
+            m = b0.mask()[0].cpu().numpy()
+            assert np.array_equal(np.packbits(m), d["masks"][masks[t]]), ("mask", t)
+            bits = b0.mask_bits()[0].cpu().numpy().view(np.uint32)
+            unpacked = ((bits[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(V, -1)
+            assert np.array_equal(unpacked[:, :b0.A].astype(bool), m)
+        pl = _np_state(b0)["vm_placement"]
+        a = pl.copy()
+        if t in acts:
+            a[acts[t][0]] = acts[t][1]
+        at = torch.tensor(a, dtype=torch.int32, device=DEV).reshape(1, V)
+        for k, b in enumerate(envs):
+            obs, rew, done, valid = b.step(at)
+            r, exp_r = float(rew[0]), d["reward"][k, t]
+            if d["rewards"][k] == "kl":
+                assert T.kl_close(r, exp_r), (t, r, exp_r)
+            else:
+                assert r == exp_r, (d["rewards"][k], t, r, exp_r)
+            if k == 0:
+                v = valid[0].cpu().numpy()
+                if t in acts:
+                    assert np.array_equal(v[acts[t][0]], acts[t][2]), ("valid", t)
+                assert int(done[0]) == d["done"][t]
+                assert obs_hash(obs[0].cpu().numpy()) == d["obs_hash"][t], ("obs", t)
+        st = _np_state(b0)
+        h = state_hash(st["vm_placement"], st["vm_cpu"], st["vm_memory"], st["cpu"],
+                       st["memory"], st["vm_remaining_runtime"])
+        assert h == d["state_hash"][t], ("state", t)
+        assert np.array_equal(b0.counters()[0].cpu().numpy(), d["counters"][t]), ("ctr", t)
+        assert np.array_equal(b0.stats()[0].cpu().numpy(), d["misc"][t]), ("misc", t)
+        if "rank" in d:
+            assert int(b0.rank()[0]) == d["rank"][t]
+
+
+@pytest.mark.parametrize("name", [n for n in T.traj_names() if n.endswith("pure")] +
+                         ["c1_10yml_ff"])
+def test_heuristic_act_hip(name):
+    from vmp.batched import BatchedVmEnv
+    d = T.load(name)
+    b = BatchedVmEnv(_cfg(d["config"]), 1, seeds=[d["config"]["seed"]], device=DEV)
+    b.eval(True)
+    acts = T.sparse_actions(d)
+    for t in range(d["T"]):
+        a = b.heuristic_act(d["policy"].replace("ff", "firstfit").replace("bf", "bestfit"))
+        an = a[0].cpu().numpy()
+        pl = _np_state(b)["vm_placement"]
+        nz = np.flatnonzero(an != pl)
+        exp = acts.get(t, (np.zeros(0, int), np.zeros(0, int), None))
+        assert np.array_equal(nz, exp[0]) and np.array_equal(an[nz], exp[1]), t
+        b.step(a)
+
+
+BATCH_CFGS = [
+    dict(pms=100, vms=300, arrival_rate=1.8182, service_length=150, reward_function="wr"),
+    dict(pms=100, vms=300, arrival_rate=0.909, service_length=1000, reward_function="kl"),
+    dict(pms=10, vms=30, arrival_rate=0.3, service_length=60, reward_function="ut"),
+    dict(pms=100, vms=1000, arrival_rate=1.8182, service_length=300, reward_function="wr"),
+    dict(pms=37, vms=130, arrival_rate=12.0, service_length=25, reward_function="kl",
+         sequence="lowuniform"),
+]
+
+
+@pytest.mark.parametrize("policy", ["firstfit", "bestfit"])
+@pytest.mark.parametrize("ci", range(len(BATCH_CFGS)))
+def test_batched_heuristic_vs_oracle(ci, policy):
+    """N envs (seeds base + 4i, incl. > 2**32) stepped by the fused act+step kernel
+    against the oracle env by env; then a fused K-step rollout continues and must
+    equal the oracle's next K steps."""
+    from vmp.batched import BatchedVmEnv
+    base = dict(training_steps=10000, eval_steps=100000, allow_null_action=True, seed=0)
+    base.update(BATCH_CFGS[ci])
+    N, steps, K = 24, 120, 60
+    seeds = np.array([7 + 4 * i for i in range(N - 2)] + [2**32 + 3, 2**40 + 11], np.int64)
+    b = BatchedVmEnv(_cfg(base), N, seeds=seeds, device=DEV)
+    b.eval(True)
+    oes = []
+    for s in seeds:
+        e = O.OracleEnv(dict(base, seed=int(s)))
+        e.eval(True)
+        e.reset(int(s))
+        oes.append(e)
+    kl = base["reward_function"] == "kl"
+    for t in range(steps):
+        obs, rew, done, valid, act = b.heuristic_step(policy, want_actions=True, want_valid=True)
+        rew, act = rew.cpu().numpy(), act.cpu().numpy()
+        obs = obs.cpu().numpy()
+        for i, e in enumerate(oes):
+            a = e.firstfit() if policy == "firstfit" else e.bestfit()
+            assert np.array_equal(a, act[i]), (t, i)
+            o, r, _, _ = e.step(a)
+            assert (T.kl_close(rew[i], r) if kl else rew[i] == r), (t, i, rew[i], r)
+            assert np.array_equal(o, obs[i]), (t, i)
+    rs, _ = b.rollout(policy, K)
+    rs = rs.cpu().numpy()
+    ctr = b.counters().cpu().numpy()
+    for i, e in enumerate(oes):
+        for k in range(K):
+            a = e.firstfit() if policy == "firstfit" else e.bestfit()
+            _, r, _, _ = e.step(a)
+            assert (T.kl_close(rs[k, i], r) if kl else rs[k, i] == r), (k, i)
+        assert np.array_equal(ctr[i], e.counters()[0]), i
+        st = _np_state(b, i)
+        assert state_hash(*[st[k] for k in ("vm_placement", "vm_cpu", "vm_memory", "cpu",
+                                             "memory", "vm_remaining_runtime")]) == \
+            state_hash(*e.state()), i
+
+
+def test_external_random_actions_vs_oracle():
+    """Dense, mostly-invalid external actions (every VM proposes every step) —
+    the many-events path of the ordered per-PM replay."""
+    from vmp.batched import BatchedVmEnv
+    base = dict(pms=20, vms=200, arrival_rate=4.0, service_length=30, training_steps=10000,
+                eval_steps=100000, allow_null_action=True, seed=0, reward_function="kl")
+    N = 16
+    seeds = np.arange(N, dtype=np.int64) * 4 + 100
+    b = BatchedVmEnv(_cfg(base), N, seeds=seeds, device=DEV)
+    oes = [O.OracleEnv(dict(base, seed=int(s))) for s in seeds]
+    for e, s in zip(oes, seeds):
+        e.reset(int(s))
+    rng = np.random.default_rng(0)
+    A = 22
+    for t in range(150):
+        acts = rng.integers(-1, A + 1, size=(N, 200))
+        obs, rew, done, valid = b.step(torch.tensor(acts, dtype=torch.int32, device=DEV))
+        rew, valid, obs = rew.cpu().numpy(), valid.cpu().numpy(), obs.cpu().numpy()
+        for i, e in enumerate(oes):
+            o, r, _, v = e.step(acts[i])
+            assert T.kl_close(rew[i], r), (t, i)
+            assert np.array_equal(v, valid[i]), (t, i)
+            assert np.array_equal(o, obs[i]), (t, i)
+
+
+def test_reset_masks_and_reseed():
+    from vmp.batched import BatchedVmEnv
+    base = dict(pms=10, vms=30, arrival_rate=0.5, service_length=20, training_steps=50,
+                eval_steps=100, allow_null_action=True, seed=0)
+    N = 8
+    b = BatchedVmEnv(_cfg(base), N, device=DEV)
+    for _ in range(60):
+        _, _, done, _, _ = b.heuristic_step("firstfit")
+    assert bool(done.all())
+    mask = torch.zeros(N, dtype=torch.bool)
+    mask[::2] = True
+    new = torch.arange(N, dtype=torch.int64) * 4 + 1000
+    b.reset(new, mask=mask)
+    ctr = b.counters().cpu().numpy()
+    assert np.all(ctr[::2, 5] == 1) and np.all(ctr[1::2, 5] == 61)
+    e = O.OracleEnv(dict(base, seed=1000))
+    e.reset(1000)
+    for t in range(30):
+        _, rew, _, _, _ = b.heuristic_step("firstfit")
+        _, r, _, _ = e.step(e.firstfit())
+        assert float(rew[0]) == r
+
+
+def test_gae_matches_reference_loop():
+    from vmp import _lib
+    Tn, N = 100, 37
+    g = torch.Generator().manual_seed(0)
+    r = torch.randn(Tn, N, generator=g)
+    d = (torch.rand(Tn, N, generator=g) < 0.05).float()
+    v = torch.randn(Tn, N, generator=g)
+    nv = torch.randn(Tn, N, generator=g)
+    adv_ref = torch.zeros(Tn, N)
+    gae = torch.zeros(N)
+    for i in reversed(range(Tn)):  # ppo.py:237-242
+        delta = r[i] + (1 - d[i]) * 0.99 * nv[i] - v[i]
+        gae = delta + (1 - d[i]) * 0.99 * 0.98 * gae
+        adv_ref[i] = gae
+    dr, dd, dv, dnv = (x.to(DEV) for x in (r, d, v, nv))
+    adv = torch.empty_like(dr)
+    ret = torch.empty_like(dr)
+    _lib.check(_lib.lib().vmp_gae(Tn, N, _lib.ptr(dr), _lib.ptr(dd), _lib.ptr(dv), _lib.ptr(dnv),
+                                  0.99, 0.98, _lib.ptr(adv), _lib.ptr(ret), None))
+    torch.cuda.synchronize()
+    assert torch.allclose(adv.cpu(), adv_ref, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(ret.cpu(), adv_ref + v, atol=1e-5, rtol=1e-5)

@@ -1,0 +1,446 @@
+// vmp_capi.cpp — extern "C" entry points of libvmp.so (declared in include/vmp.h).
+// Host-side: argument checks, device allocation, per-config constants
+// (Poisson setup evaluated with glibc exactly as numpy's C code does), LDS
+// carve-out, and kernel dispatch on the handle's stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vmp.h"
+#include "vmp_layout.h"
+
+namespace vmp {
+template <int VPT>
+__global__ void k_env(EnvParams p, StepOut o);
+__global__ void k_reset(EnvParams p, const int64_t *seeds, const uint8_t *env_mask, float *obs);
+__global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double *vm_mem,
+                         double *cpu, double *mem, int64_t *remaining, int64_t *rank);
+__global__ void k_counters(EnvParams p, int64_t *ctr, double *st);
+__global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, uint8_t *mask);
+__global__ void k_gae(int T, int N, const float *r, const float *d, const float *v,
+                      const float *nv, float gamma, float lam, float *adv, float *ret);
+__global__ void k_masked_sample(int B, int V, int A, int W, const float *logits,
+                                const uint32_t *bits, uint64_t seed, uint64_t offset,
+                                int32_t *action, float *lp_row, float *ent_row);
+}  // namespace vmp
+
+using namespace vmp;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t _e = (expr);                                                        \
+    if (_e != hipSuccess)                                                          \
+      return fail(_e == hipErrorOutOfMemory ? VMP_EOOM : VMP_EDEVICE,              \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));              \
+  } while (0)
+
+// random_loggam (numpy distributions.c), host copy for the PTRS table.
+double loggam_host(double x) {
+  static const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03,
+                               7.936507936507937e-04, -5.952380952380952e-04,
+                               8.417508417508418e-04, -1.917526917526918e-03,
+                               6.410256410256410e-03, -2.955065359477124e-02,
+                               1.796443723688307e-01, -1.39243221690590e+00};
+  if (x == 1.0 || x == 2.0) return 0.0;
+  int64_t n = (x < 7.0) ? (int64_t)(7 - x) : 0;
+  double x0 = x + n;
+  double x2 = (1.0 / x0) * (1.0 / x0);
+  double gl0 = a[9];
+  for (int k = 8; k >= 0; k--) {
+    gl0 *= x2;
+    gl0 += a[k];
+  }
+  double gl = gl0 / x0 + 0.5 * 1.8378770664093453e+00 + (x0 - 0.5) * std::log(x0) - x0;
+  if (x < 7.0)
+    for (int64_t k = 1; k <= n; k++) {
+      gl -= std::log(x0 - 1.0);
+      x0 -= 1.0;
+    }
+  return gl;
+}
+
+}  // namespace
+
+struct vmp_handle {
+  vmp_config cfg;
+  int32_t N, P, V, A, D, W32, vpt;
+  int32_t device;
+  int32_t eval_mode;
+  hipStream_t stream;
+  uint64_t *vmw;
+  double *pm;
+  EnvHdr *hdr;
+  double *lg_arr, *lg_svc;
+  PoisConst arr, svc;
+  EnvParams prm;
+  uint32_t *scratch_bits;  // for vmp_mask_bool
+};
+
+namespace {
+
+int setup_pois(double lam, PoisConst &c, double **dev_tab, std::vector<double> &host_tab) {
+  std::memset(&c, 0, sizeof(c));
+  c.lam = lam;
+  if (lam == 0) {
+    c.kind = 0;
+  } else if (lam < 10) {
+    c.kind = 1;
+    c.enlam = std::exp(-lam);
+  } else {
+    c.kind = 2;
+    double slam = std::sqrt(lam);
+    c.loglam = std::log(lam);
+    c.b = 0.931 + 2.53 * slam;
+    c.a = -0.059 + 0.02483 * c.b;
+    c.invalpha = 1.1239 + 1.1328 / (c.b - 3.4);
+    c.vr = 0.9277 - 3.6224 / (c.b - 2);
+    c.log_invalpha = std::log(c.invalpha);
+    int64_t n = (int64_t)(lam + 16.0 * slam + 64.0);
+    if (n > (1 << 22)) n = 1 << 22;
+    host_tab.resize((size_t)n);
+    for (int64_t k = 0; k < n; k++) host_tab[(size_t)k] = loggam_host((double)k);
+    c.tab_n = (int32_t)n;
+    HIP_TRY(hipMalloc(dev_tab, sizeof(double) * n));
+    HIP_TRY(hipMemcpy(*dev_tab, host_tab.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+    c.loggam_tab = *dev_tab;
+  }
+  return VMP_OK;
+}
+
+inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+
+void carve(vmp_handle *h) {
+  EnvParams &p = h->prm;
+  int64_t off = 0;
+  const int P = h->P, V = h->V;
+  p.off_pm = (int32_t)off;
+  off = align16(off + 16 * (int64_t)P);
+  p.off_fpm = (int32_t)off;
+  off = align16(off + 12 * (int64_t)P);  // fcpu, fmem, fkey
+  p.off_ord = (int32_t)off;
+  off = align16(off + 2 * (int64_t)P + 2 * (int64_t)V);  // ord + acts
+  p.off_list = (int32_t)off;
+  off = align16(off + 4 * (int64_t)V);
+  p.off_ccomp = (int32_t)off;
+  off = align16(off + V);
+  p.off_mcomp = (int32_t)off;
+  off = align16(off + V);
+  int nl = V / 32 + 8;
+  p.off_leaf = (int32_t)off;
+  off = align16(off + 4 * (2 * (int64_t)nl + 96));
+  p.off_tmp = (int32_t)off;
+  off = align16(off + 8 * ((int64_t)nl + 32));
+  p.lds_wave_bytes = (int32_t)off;
+}
+
+int launch_env(vmp_handle *h, const StepOut &o) {
+  dim3 grid((h->N + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
+  size_t lds = (size_t)h->prm.lds_wave_bytes * kWavesPerBlock;
+  switch (h->vpt) {
+    case 1: hipLaunchKernelGGL(k_env<1>, grid, block, lds, h->stream, h->prm, o); break;
+    case 2: hipLaunchKernelGGL(k_env<2>, grid, block, lds, h->stream, h->prm, o); break;
+    case 4: hipLaunchKernelGGL(k_env<4>, grid, block, lds, h->stream, h->prm, o); break;
+    case 8: hipLaunchKernelGGL(k_env<8>, grid, block, lds, h->stream, h->prm, o); break;
+    default: hipLaunchKernelGGL(k_env<16>, grid, block, lds, h->stream, h->prm, o); break;
+  }
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+StepOut empty_out() {
+  StepOut o;
+  std::memset(&o, 0, sizeof(o));
+  o.policy = -1;
+  return o;
+}
+
+void refresh_params(vmp_handle *h) {
+  h->prm.eval_mode = h->eval_mode;
+  h->prm.limit = h->eval_mode ? h->cfg.eval_steps : h->cfg.training_steps;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vmp_abi_version(void) { return VMP_ABI_VERSION; }
+const char *vmp_last_error(void) { return g_err.c_str(); }
+
+int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32_t device,
+               vmp_handle **out) {
+  if (!cfg || !out || n_env <= 0 || !seeds) return fail(VMP_EINVAL, "null argument or n_env <= 0");
+  if (cfg->pms < 1 || cfg->pms > 65533) return fail(VMP_EINVAL, "pms must be in [1, 65533]");
+  if (cfg->vms < 1 || cfg->vms > kMaxVPT * kWaveSize)
+    return fail(VMP_EINVAL, "vms must be in [1, 1024] on this build");
+  if (cfg->reward_function < 0 || cfg->reward_function > 2)
+    return fail(VMP_EINVAL, "Function does not exist: reward_function");  // env.py:156
+  if (cfg->sequence < 0 || cfg->sequence > 2) return fail(VMP_EINVAL, "unknown sequence");
+  if (!(cfg->arrival_rate >= 0) || !(cfg->service_length >= 0))
+    return fail(VMP_EINVAL, "arrival_rate and service_length must be >= 0");
+  for (int32_t i = 0; i < n_env; i++)
+    if (seeds[i] < 0) return fail(VMP_EINVAL, "seeds must be non-negative");
+  HIP_TRY(hipSetDevice(device));
+  vmp_handle *h = new vmp_handle();
+  std::memset(h, 0, sizeof(*h));
+  h->cfg = *cfg;
+  h->N = n_env;
+  h->P = cfg->pms;
+  h->V = cfg->vms;
+  h->A = cfg->allow_null_action ? cfg->pms + 2 : cfg->pms + 1;
+  h->D = 3 * cfg->vms + 2 * cfg->pms;
+  h->W32 = (h->A + 31) / 32;
+  int need = (h->V + 63) / 64;
+  h->vpt = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : need <= 8 ? 8 : 16;
+  h->device = device;
+  h->stream = nullptr;
+  std::vector<double> t1, t2;
+  int rc = setup_pois(cfg->arrival_rate, h->arr, &h->lg_arr, t1);
+  if (rc == VMP_OK) rc = setup_pois(cfg->service_length, h->svc, &h->lg_svc, t2);
+  if (rc != VMP_OK) {
+    delete h;
+    return rc;
+  }
+  hipError_t e1 = hipMalloc(&h->vmw, sizeof(uint64_t) * (size_t)n_env * h->V);
+  hipError_t e2 = hipMalloc(&h->pm, sizeof(double) * (size_t)n_env * 2 * h->P);
+  hipError_t e3 = hipMalloc(&h->hdr, sizeof(EnvHdr) * (size_t)n_env);
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+    vmp_destroy(h);
+    return fail(VMP_EOOM, "device allocation failed");
+  }
+  HIP_TRY(hipMemset(h->hdr, 0, sizeof(EnvHdr) * (size_t)n_env));
+  EnvParams &p = h->prm;
+  p.N = h->N;
+  p.P = h->P;
+  p.V = h->V;
+  p.A = h->A;
+  p.D = h->D;
+  p.W32 = h->W32;
+  p.reward = cfg->reward_function;
+  p.cap_target_util = cfg->cap_target_util;
+  int64_t M = cfg->training_steps > cfg->eval_steps ? cfg->training_steps : cfg->eval_steps;
+  p.M2 = 2 * M;
+  p.beta = cfg->beta;
+  p.seq_lo = cfg->sequence == VMP_SEQ_HIGHUNIFORM ? 0.25 : 0.1;
+  double hi = cfg->sequence == VMP_SEQ_LOWUNIFORM ? 0.65 : 1.0;
+  p.seq_range = hi - p.seq_lo;  // Generator.uniform: low + (high-low)*u
+  p.arr = h->arr;
+  p.svc = h->svc;
+  p.vmw = h->vmw;
+  p.pm = h->pm;
+  p.hdr = h->hdr;
+  carve(h);
+  if (p.lds_wave_bytes * kWavesPerBlock > 160 * 1024 - 2048) {
+    vmp_destroy(h);
+    return fail(VMP_EINVAL, "config too large for the LDS-resident kernel");
+  }
+  refresh_params(h);
+  int64_t *dseeds = nullptr;
+  HIP_TRY(hipMalloc(&dseeds, sizeof(int64_t) * n_env));
+  HIP_TRY(hipMemcpy(dseeds, seeds, sizeof(int64_t) * n_env, hipMemcpyHostToDevice));
+  dim3 grid((n_env + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
+  hipLaunchKernelGGL(k_reset, grid, block, 0, h->stream, h->prm, dseeds, nullptr, nullptr);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipFree(dseeds));
+  *out = h;
+  return VMP_OK;
+}
+
+int vmp_destroy(vmp_handle *h) {
+  if (!h) return VMP_OK;
+  (void)hipFree(h->vmw);
+  (void)hipFree(h->pm);
+  (void)hipFree(h->hdr);
+  (void)hipFree(h->lg_arr);
+  (void)hipFree(h->lg_svc);
+  (void)hipFree(h->scratch_bits);
+  delete h;
+  return VMP_OK;
+}
+
+int vmp_set_stream(vmp_handle *h, void *s) {
+  if (!h) return fail(VMP_EINVAL, "null handle");
+  h->stream = (hipStream_t)s;
+  return VMP_OK;
+}
+
+int vmp_set_eval(vmp_handle *h, int32_t eval_mode) {
+  if (!h) return fail(VMP_EINVAL, "null handle");
+  h->eval_mode = eval_mode ? 1 : 0;
+  refresh_params(h);
+  return VMP_OK;
+}
+
+int vmp_dims(const vmp_handle *h, int32_t *n, int32_t *P, int32_t *V, int32_t *A, int32_t *D) {
+  if (!h) return fail(VMP_EINVAL, "null handle");
+  if (n) *n = h->N;
+  if (P) *P = h->P;
+  if (V) *V = h->V;
+  if (A) *A = h->A;
+  if (D) *D = h->D;
+  return VMP_OK;
+}
+
+int vmp_reset(vmp_handle *h, const int64_t *seeds, const uint8_t *env_mask, float *obs) {
+  if (!h) return fail(VMP_EINVAL, "null handle");
+  dim3 grid((h->N + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
+  hipLaunchKernelGGL(k_reset, grid, block, 0, h->stream, h->prm, seeds, env_mask, obs);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward, uint8_t *done,
+             uint8_t *valid) {
+  if (!h || !actions) return fail(VMP_EINVAL, "null handle or actions");
+  StepOut o = empty_out();
+  o.actions = actions;
+  o.obs = obs;
+  o.reward = reward;
+  o.done = done;
+  o.valid = valid;
+  o.k_steps = 1;
+  return launch_env(h, o);
+}
+
+int vmp_heuristic_act(vmp_handle *h, int32_t policy, int32_t *actions) {
+  if (!h || !actions) return fail(VMP_EINVAL, "null handle or actions");
+  if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
+    return fail(VMP_EINVAL, "unknown policy");
+  StepOut o = empty_out();
+  o.policy = policy;
+  o.act_out = actions;
+  o.k_steps = 0;
+  return launch_env(h, o);
+}
+
+int vmp_heuristic_step(vmp_handle *h, int32_t policy, int32_t *actions_out, float *obs,
+                       double *reward, uint8_t *done, uint8_t *valid) {
+  if (!h) return fail(VMP_EINVAL, "null handle");
+  if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
+    return fail(VMP_EINVAL, "unknown policy");
+  StepOut o = empty_out();
+  o.policy = policy;
+  o.act_out = actions_out;
+  o.obs = obs;
+  o.reward = reward;
+  o.done = done;
+  o.valid = valid;
+  o.k_steps = 1;
+  return launch_env(h, o);
+}
+
+int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double *rewards,
+                          int64_t *done_count) {
+  if (!h || k_steps < 1) return fail(VMP_EINVAL, "null handle or k_steps < 1");
+  if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
+    return fail(VMP_EINVAL, "unknown policy");
+  StepOut o = empty_out();
+  o.policy = policy;
+  o.reward = rewards;
+  o.done_count = done_count;
+  o.k_steps = k_steps;
+  return launch_env(h, o);
+}
+
+int vmp_mask(vmp_handle *h, uint32_t *bits) {
+  if (!h || !bits) return fail(VMP_EINVAL, "null argument");
+  StepOut o = empty_out();
+  o.mask_bits = bits;
+  return launch_env(h, o);
+}
+
+int vmp_mask_bool(vmp_handle *h, uint8_t *mask) {
+  if (!h || !mask) return fail(VMP_EINVAL, "null argument");
+  if (!h->scratch_bits)
+    HIP_TRY(hipMalloc(&h->scratch_bits, sizeof(uint32_t) * (size_t)h->N * h->V * h->W32));
+  int rc = vmp_mask(h, h->scratch_bits);
+  if (rc) return rc;
+  int64_t rows = (int64_t)h->N * h->V;
+  int64_t n = rows * h->A;
+  hipLaunchKernelGGL(k_mask_bool, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
+                     rows, h->A, h->W32, h->scratch_bits, mask);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_get_obs(vmp_handle *h, float *obs) {
+  if (!h || !obs) return fail(VMP_EINVAL, "null argument");
+  StepOut o = empty_out();
+  o.obs = obs;
+  return launch_env(h, o);
+}
+
+int vmp_get_counters(vmp_handle *h, int64_t *counters) {
+  if (!h || !counters) return fail(VMP_EINVAL, "null argument");
+  hipLaunchKernelGGL(k_counters, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,
+                     counters, nullptr);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_get_stats(vmp_handle *h, double *stats) {
+  if (!h || !stats) return fail(VMP_EINVAL, "null argument");
+  hipLaunchKernelGGL(k_counters, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,
+                     nullptr, stats);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_get_state(vmp_handle *h, int64_t *placement, double *vm_cpu, double *vm_mem,
+                  double *cpu, double *mem, int64_t *remaining) {
+  if (!h) return fail(VMP_EINVAL, "null handle");
+  int64_t n = (int64_t)h->N * (h->V > h->P ? h->V : h->P);
+  hipLaunchKernelGGL(k_export, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
+                     h->prm, placement, vm_cpu, vm_mem, cpu, mem, remaining, nullptr);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_get_rank(vmp_handle *h, int64_t *rank) {
+  if (!h || !rank) return fail(VMP_EINVAL, "null argument");
+  hipLaunchKernelGGL(k_export, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,
+                     nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, rank);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const float *value,
+            const float *next_value, float gamma, float lam, float *adv, float *ret,
+            void *stream) {
+  if (T < 0 || N < 0 || !reward || !done || !value || !next_value || !adv || !ret)
+    return fail(VMP_EINVAL, "bad gae arguments");
+  if (T == 0 || N == 0) return VMP_OK;
+  hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, T, N,
+                     reward, done, value, next_value, gamma, lam, adv, ret);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
+                      const uint32_t *mask_bits, uint64_t seed, uint64_t offset, int32_t *action,
+                      float *logprob_row, float *entropy_row, void *stream) {
+  if (B < 0 || V < 1 || A < 1 || !logits || !action || !logprob_row || !entropy_row)
+    return fail(VMP_EINVAL, "bad sample arguments");
+  int64_t rows = (int64_t)B * V;
+  if (rows == 0) return VMP_OK;
+  int W = (A + 31) / 32;
+  hipLaunchKernelGGL(k_masked_sample, dim3((unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock)),
+                     dim3(64 * kWavesPerBlock), 0, (hipStream_t)stream, B, V, A, W, logits,
+                     mask_bits, seed, offset, action, logprob_row, entropy_row);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+// vmp_layout.h — device-resident state layout and launch parameters shared by
+// the HIP kernels (vmp_kernels.hip) and the C-ABI host side (vmp_capi.cpp).
+//
+// HBM layout, env-major so one wavefront streams one env's state with
+// coalesced 64-lane accesses (one wave per env):
+//
+//   vmw  u64 [N][V]   one word per VM slot (env.py:186-196 state, 8 B/VM):
+//                       bits  0..15 placement (0..P-1 PM, P = WAIT, P+1 = NULL)
+//                       bits 16..23 vm_cpu in hundredths (np.around(.,2) makes
+//                                   every size k/100 exactly, env.py:212-219)
+//                       bits 24..31 vm_memory in hundredths
+//                       bits 32..63 remaining runtime (env.py:290)
+//   pm   f64 [N][2][P] cpu[P] then memory[P]; kept in f64 because their values
+//                       carry the reference's accumulated rounding history
+//   hdr  EnvHdr [N]    256 B: 4 PCG64 streams, sequence bases, counters, stats
+//
+// vm_suspended / vm_planned_runtime are never read on the path (SURVEY App. B
+// item 14) and are not stored.
+#pragma once
+#include <stdint.h>
+
+namespace vmp {
+
+constexpr int kWaveSize = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kMaxVPT = 16;  // VM slots per lane held in registers: V <= 1024
+
+struct alignas(16) EnvHdr {
+  uint64_t rng[4][4];      // [stream][state_hi, state_lo, inc_hi, inc_lo]; rng1..rng4
+  uint64_t seqbase[2][2];  // rng1/rng2 state at the last reset (sequence element 0)
+  int64_t timestep;
+  int64_t total_requests, served, suspend_action, place_action, dropped;
+  double total_cpu_req, total_mem_req, waiting_ratio, tcm, tmm;
+  int64_t pad;
+};
+static_assert(sizeof(EnvHdr) == 256, "EnvHdr must be 256 B");
+
+// Poisson(lam) constants (distributions.c random_poisson), computed on the host
+// with glibc so the device only evaluates per-draw terms.
+struct PoisConst {
+  double lam, enlam;                         // mult method (lam < 10)
+  double loglam, b, a, invalpha, vr, log_invalpha;  // PTRS (lam >= 10)
+  const double *loggam_tab;                  // loggam(k+1) for k in [0, tab_n)
+  int32_t kind;                              // 0: lam == 0, 1: mult, 2: PTRS
+  int32_t tab_n;
+};
+
+struct EnvParams {
+  int32_t N, P, V, A, D, W32;  // W32 = ceil(A/32) mask words per VM row
+  int32_t reward, cap_target_util, eval_mode, pad0;
+  int64_t limit;          // eval_steps if eval_mode else training_steps
+  int64_t M2;             // 2 * max(training_steps, eval_steps)
+  double beta, seq_lo, seq_range;
+  PoisConst arr, svc;     // arrivals (rng3), service lengths (rng4)
+  uint64_t *vmw;
+  double *pm;
+  EnvHdr *hdr;
+  // per-wave LDS carve (bytes); offsets inside one wave's region
+  int32_t lds_wave_bytes;
+  int32_t off_pm, off_fpm, off_ord, off_list, off_ccomp, off_mcomp, off_tmp, off_leaf;
+};
+
+struct StepOut {
+  const int32_t *actions;  // external actions [N][V] or null (heuristic)
+  int32_t *act_out;        // [N][V] nullable
+  float *obs;              // [N][D] nullable (final state)
+  double *reward;          // [K][N] nullable
+  uint8_t *done;           // [N] nullable (last step)
+  int64_t *done_count;     // [N] nullable
+  uint8_t *valid;          // [N][V] nullable (last step)
+  uint32_t *mask_bits;     // [N][V][W32] nullable (final state)
+  int32_t policy;          // -1 external, 0 first-fit, 1 best-fit
+  int32_t k_steps;
+};
+
+}  // namespace vmp
