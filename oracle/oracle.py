@@ -72,6 +72,7 @@ def lib():
             "oracle_pcg_advance_raw": (u64, [u64, u64]),
             "oracle_pw_sum": (dbl, [P, i64]), "oracle_argsort_f32": (None, [P, i64, P]),
             "oracle_rollout": (i64, [P, i32, i64, i64, i64, i32, i32, i32, P, P]),
+            "oracle_rollout_timed": (dbl, [P, i32, i64, i64, i64, i64, i32, i32, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -163,3 +164,13 @@ def rollout(cfg: dict, n_env, seed0, stride, steps, policy=0, eval_mode=True, th
     lib().oracle_rollout(ctypes.byref(c), n_env, seed0, stride, steps, policy, int(eval_mode),
                          threads, _p(rs), _p(ctr))
     return rs, ctr
+
+
+def rollout_timed(cfg: dict, n_env, seed0, stride, warmup, steps, policy=0, threads=1):
+    """Warm-started timed CPU rollout (bench.py cpu_baseline). Returns
+    (seconds, reward_sum[n_env])."""
+    c = make_config(cfg)
+    rs = np.zeros(n_env)
+    sec = lib().oracle_rollout_timed(ctypes.byref(c), n_env, seed0, stride, warmup, steps,
+                                     policy, threads, _p(rs))
+    return sec, rs

@@ -765,3 +765,54 @@ int64_t oracle_rollout(const vmp_config *cfg, int32_t n_env, int64_t seed0, int6
   }
   return (int64_t)n_env * steps;
 }
+
+/* CPU baseline timing: n_env envs on n_threads threads; `warmup` untimed
+ * act+step iterations per env, then `steps` timed ones (wall time of the
+ * parallel region between two barriers). Returns seconds. */
+#include <omp.h>
+double oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0, int64_t stride,
+                            int64_t warmup, int64_t steps, int32_t policy, int32_t n_threads,
+                            double *reward_sum) {
+  oenv **envs = (oenv **)calloc(n_env, sizeof(oenv *));
+  double t0 = 0, t1 = 0;
+#pragma omp parallel num_threads(n_threads)
+  {
+    int64_t *act = (int64_t *)malloc(sizeof(int64_t) * cfg->vms);
+#pragma omp for schedule(static)
+    for (int32_t i = 0; i < n_env; i++) {
+      vmp_config c = *cfg;
+      c.seed = seed0 + stride * (int64_t)i;
+      envs[i] = oracle_create(&c);
+      oracle_set_eval(envs[i], 1);
+      for (int64_t s = 0; s < warmup; s++) {
+        if (policy == VMP_POLICY_BESTFIT) oracle_bestfit(envs[i], act);
+        else oracle_firstfit(envs[i], act);
+        double r;
+        int term;
+        oracle_step(envs[i], act, NULL, &r, &term);
+      }
+    }
+#pragma omp barrier
+#pragma omp single
+    t0 = omp_get_wtime();
+#pragma omp for schedule(static)
+    for (int32_t i = 0; i < n_env; i++) {
+      double rs = 0.0;
+      for (int64_t s = 0; s < steps; s++) {
+        if (policy == VMP_POLICY_BESTFIT) oracle_bestfit(envs[i], act);
+        else oracle_firstfit(envs[i], act);
+        double r;
+        int term;
+        oracle_step(envs[i], act, NULL, &r, &term);
+        rs += r;
+      }
+      if (reward_sum) reward_sum[i] = rs;
+    }
+#pragma omp single
+    t1 = omp_get_wtime();
+    free(act);
+  }
+  for (int32_t i = 0; i < n_env; i++) oracle_destroy(envs[i]);
+  free(envs);
+  return t1 - t0;
+}
