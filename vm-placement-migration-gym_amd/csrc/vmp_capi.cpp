@@ -86,6 +86,7 @@ struct vmp_handle {
   PoisConst arr, svc;
   EnvParams prm;
   uint32_t *scratch_bits;  // for vmp_mask_bool
+  PoisConst *pois_dev;
 };
 
 namespace {
@@ -121,27 +122,54 @@ int setup_pois(double lam, PoisConst &c, double **dev_tab, std::vector<double> &
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
+// Max recursion depth of numpy's pairwise split for n <= V (kernel limit 5).
+int pw_depth(int n) {
+  if (n <= 128) return 0;
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  int a = pw_depth(n2), b = pw_depth(n - n2);
+  return 1 + (a > b ? a : b);
+}
+int pw_leaves(int n) {
+  if (n <= 128) return 1;
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_leaves(n2) + pw_leaves(n - n2);
+}
+
 void carve(vmp_handle *h) {
   EnvParams &p = h->prm;
+  const int64_t P = h->P, V = h->V;
+  int max_leaves = 1;
+  for (int n = 0; n <= V || n <= P; n++) {
+    int l = pw_leaves(n);
+    if (l > max_leaves) max_leaves = l;
+  }
+  p.NW = (int32_t)((P + 63) / 64);
+  p.n_leaf = max_leaves + 8;
   int64_t off = 0;
-  const int P = h->P, V = h->V;
+  p.off_hdr = (int32_t)off;
+  off = align16(off + (int64_t)sizeof(EnvHdr));
   p.off_pm = (int32_t)off;
-  off = align16(off + 16 * (int64_t)P);
+  off = align16(off + 16 * P);           // cpu, mem f64
   p.off_fpm = (int32_t)off;
-  off = align16(off + 12 * (int64_t)P);  // fcpu, fmem, fkey
+  off = align16(off + 12 * P);           // fcpu, fmem, fkey f32
+  p.off_thr = (int32_t)off;
+  off = align16(off + 2 * P);            // tc, tm u8
   p.off_ord = (int32_t)off;
-  off = align16(off + 2 * (int64_t)P + 2 * (int64_t)V);  // ord + acts
-  p.off_list = (int32_t)off;
-  off = align16(off + 4 * (int64_t)V);
+  off = align16(off + 2 * P);            // BF visiting order u16
+  p.off_bits = (int32_t)off;
+  off = align16(off + 2 * 101 * 8 * (int64_t)p.NW);  // bc, bm
+  p.off_sort = (int32_t)off;
+  off = align16(off + 4 * 256);          // introsort stacks
+  p.off_stage = (int32_t)off;
+  off = align16(off + 8 * 64);           // staged accepted VMs
   p.off_ccomp = (int32_t)off;
-  off = align16(off + V);
-  p.off_mcomp = (int32_t)off;
-  off = align16(off + V);
-  int nl = V / 32 + 8;
+  off = align16(off + 2 * V);            // ccomp, mcomp u8
   p.off_leaf = (int32_t)off;
-  off = align16(off + 4 * (2 * (int64_t)nl + 96));
-  p.off_tmp = (int32_t)off;
-  off = align16(off + 8 * ((int64_t)nl + 32));
+  off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);  // lo, len, lane-0 stack
+  p.off_leafval = (int32_t)off;
+  off = align16(off + 8 * 8 * (int64_t)p.n_leaf + 8 * (2 * (int64_t)p.n_leaf + 64));
   p.lds_wave_bytes = (int32_t)off;
 }
 
@@ -237,10 +265,23 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   p.seq_range = hi - p.seq_lo;  // Generator.uniform: low + (high-low)*u
   p.arr = h->arr;
   p.svc = h->svc;
+  {
+    PoisConst pc[2] = {h->arr, h->svc};
+    HIP_TRY(hipMalloc(&h->pois_dev, sizeof(pc)));
+    HIP_TRY(hipMemcpy(h->pois_dev, pc, sizeof(pc), hipMemcpyHostToDevice));
+    p.pois = h->pois_dev;
+  }
   p.vmw = h->vmw;
   p.pm = h->pm;
   p.hdr = h->hdr;
   carve(h);
+  int maxn = h->V > h->P ? h->V : h->P;
+  int depth = 0;
+  for (int n = 0; n <= maxn; n++) depth = pw_depth(n) > depth ? pw_depth(n) : depth;
+  if (depth > 5) {
+    vmp_destroy(h);
+    return fail(VMP_EINVAL, "config exceeds the pairwise-sum recursion depth of this build");
+  }
   if (p.lds_wave_bytes * kWavesPerBlock > 160 * 1024 - 2048) {
     vmp_destroy(h);
     return fail(VMP_EINVAL, "config too large for the LDS-resident kernel");
@@ -266,6 +307,7 @@ int vmp_destroy(vmp_handle *h) {
   (void)hipFree(h->lg_arr);
   (void)hipFree(h->lg_svc);
   (void)hipFree(h->scratch_bits);
+  (void)hipFree(h->pois_dev);
   delete h;
   return VMP_OK;
 }

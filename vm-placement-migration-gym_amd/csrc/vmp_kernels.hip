@@ -16,6 +16,12 @@
 
 #include "vmp_layout.h"
 
+// Minimum waves per SIMD the env kernel is register-allocated for
+// (__launch_bounds__ 2nd argument); measured choice, see DESIGN.md.
+#ifndef VMP_WAVES_PER_EU
+#define VMP_WAVES_PER_EU 1
+#endif
+
 namespace vmp {
 
 // ------------------------------------------------------------ wave utils --
@@ -126,7 +132,7 @@ __device__ void pcg_seed(Pcg &r, uint64_t seed) {
 }
 
 // random_loggam (distributions.c) — device fallback outside the host table.
-__device__ double loggam_dev(double x) {
+__device__ __forceinline__ double loggam_dev(double x) {
   const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
                         -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
                         6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
@@ -150,7 +156,7 @@ __device__ double loggam_dev(double x) {
 }
 
 // random_poisson (distributions.c): mult method (lam < 10) / PTRS (lam >= 10).
-__device__ int64_t poisson(Pcg &r, const PoisConst &c) {
+__device__ __forceinline__ int64_t poisson(Pcg &r, const PoisConst &c) {
   if (c.kind == 2) {
     for (;;) {
       double U = next_double(r) - 0.5;
@@ -177,136 +183,146 @@ __device__ int64_t poisson(Pcg &r, const PoisConst &c) {
   }
 }
 
-// ---------------------------------------------------- pairwise summation --
-// numpy DOUBLE_pairwise_sum (loops_utils.h.src, PW_BLOCKSIZE 128) over
-// f(0..n-1), evaluated by one wave. Leaves (<= 128 elements, 8 interleaved
-// accumulators + sequential tail) are computed 8 per pass by lane groups of 8;
-// the recursion n2 = n/2 - (n/2)%8 is replayed by a wave-uniform stack
-// machine. `scr` is a per-wave LDS scratch of >= 3*(#leaves + 64) words.
-struct PwScratch {
-  int32_t *lo, *len;  // leaf list
-  double *val;        // leaf sums
-  int32_t *stk;       // DFS stack (o, n, phase) triples
-  double *vstk;       // value stack
-};
-
-template <class F>
-__device__ __forceinline__ double pw_leaf_group(int o, int m, int j, F &f, int lane) {
-  // lanes j = lane&7 of a group: accumulator chain j, then lane j==0 combines.
-  double r = 0.0;
-  int full = m - (m % 8);
-  if (m >= 8) {
-    r = f(o + j);
-    for (int i = o + j + 8; i < o + full; i += 8) r += f(i);
+// Out of line: one Poisson draw from stream k of the wave's LDS header (all
+// lanes call it with identical state; lane 0 writes the advanced state back).
+__device__ __forceinline__ int64_t poisson_lds(uint64_t *hdr_rng, const PoisConst *c) {
+  Pcg r;
+  r.s = U128{hdr_rng[0], hdr_rng[1]};
+  r.inc = U128{hdr_rng[2], hdr_rng[3]};
+  const int64_t x = poisson(r, *c);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if ((threadIdx.x & 63) == 0) {
+    hdr_rng[0] = r.s.hi;
+    hdr_rng[1] = r.s.lo;
   }
-  int base = lane & ~7;
-  double r0 = __shfl(r, base + 0), r1 = __shfl(r, base + 1), r2 = __shfl(r, base + 2),
-         r3 = __shfl(r, base + 3), r4 = __shfl(r, base + 4), r5 = __shfl(r, base + 5),
-         r6 = __shfl(r, base + 6), r7 = __shfl(r, base + 7);
-  double res;
-  int i0;
-  if (m < 8) {
-    res = 0.0;
-    i0 = o;
-  } else {
-    res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    i0 = o + full;
-  }
-  for (int i = i0; i < o + m; i++) res += f(i);
-  return res;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return x;
 }
 
-template <class F>
-__device__ double wave_pw_sum(int n, F f, const PwScratch &S) {
-  const int lane = lane_id();
-  if (n <= 128) {
-    // single leaf: every group computes it, all lanes hold the result
-    return pw_leaf_group(0, n, lane & 7, f, lane);
-  }
-  // 1) enumerate leaves in DFS (left-first) order
-  int nleaf = 0, sp = 0;
+// ---------------------------------------------------- pairwise summation --
+// numpy DOUBLE_pairwise_sum (loops_utils.h.src, PW_BLOCKSIZE 128) of
+// f(0..n-1) by one wave. Leaves (<= 128 elements: 8 interleaved accumulator
+// chains, an ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) combine, a sequential tail)
+// run lane-parallel (8 lanes per leaf); the split n2 = n/2 - (n/2)%8 is
+// enumerated and the partial sums combined by lane 0 alone on small LDS
+// stacks, so no cross-lane hand-off happens inside the recursion.
+struct PwLds {
+  int32_t *lo, *len;  // leaf list (DFS order), n_leaf entries
+  int32_t *stk;       // lane-0 stack, 3 * 64 ints
+  double *acc;        // 8 accumulators per leaf
+  double *val;        // leaf sums, + value stack
+};
+
+// lane 0 only: leaves of the recursion for n, left to right.
+__device__ __forceinline__ int pw_plan(int n, const PwLds &S) {
+  int sp = 0, nl = 0;
   S.stk[0] = 0;
   S.stk[1] = n;
-  sp = 1;
-  wsync();
+  sp = 2;
   while (sp > 0) {
-    sp--;
-    int o = S.stk[2 * sp], m = S.stk[2 * sp + 1];
-    wsync();
+    sp -= 2;
+    const int o = S.stk[sp], m = S.stk[sp + 1];
     if (m <= 128) {
-      if (lane == 0) {
-        S.lo[nleaf] = o;
-        S.len[nleaf] = m;
-      }
-      nleaf++;
+      S.lo[nl] = o;
+      S.len[nl] = m;
+      nl++;
     } else {
       int n2 = m / 2;
       n2 -= n2 % 8;
-      if (lane == 0) {  // push right then left: left is popped first
-        S.stk[2 * sp] = o + n2;
-        S.stk[2 * sp + 1] = m - n2;
-        S.stk[2 * sp + 2] = o;
-        S.stk[2 * sp + 3] = n2;
-      }
-      sp += 2;
+      S.stk[sp] = o + n2;  // right, popped second
+      S.stk[sp + 1] = m - n2;
+      S.stk[sp + 2] = o;   // left, popped first
+      S.stk[sp + 3] = n2;
+      sp += 4;
     }
-    wsync();
   }
-  // 2) leaf sums, 8 leaves per pass
-  for (int b = 0; b < nleaf; b += 8) {
-    int l = b + (lane >> 3);
-    int o = 0, m = 0;
-    if (l < nleaf) {
-      o = S.lo[l];
-      m = S.len[l];
-    }
-    double v = pw_leaf_group(o, m, lane & 7, f, lane);
-    if (l < nleaf && (lane & 7) == 0) S.val[l] = v;
-  }
-  wsync();
-  // 3) replay the recursion combining leaf sums: stack of (o, n, phase)
-  int leaf = 0, vsp = 0;
-  sp = 0;
-  S.stk[0] = 0;
-  S.stk[1] = n;
-  S.stk[2] = 0;
-  sp = 1;
-  wsync();
+  return nl;
+}
+
+// lane 0 only: pw(n) = pw(n2) + pw(n - n2) over the leaf sums in val[].
+__device__ __forceinline__ double pw_combine(int n, const PwLds &S, int nl) {
+  double *vs = S.val + nl;  // value stack after the leaf sums
+  int sp = 0, vsp = 0, leaf = 0;
+  S.stk[0] = n;
+  S.stk[1] = 0;
+  sp = 2;
   while (sp > 0) {
-    sp--;
-    int o = S.stk[3 * sp], m = S.stk[3 * sp + 1], ph = S.stk[3 * sp + 2];
-    wsync();
+    sp -= 2;
+    const int m = S.stk[sp], ph = S.stk[sp + 1];
     if (m <= 128) {
-      double v = S.val[leaf++];
-      if (lane == 0) S.vstk[vsp] = v;
-      vsp++;
+      vs[vsp++] = S.val[leaf++];
     } else if (ph == 0) {
       int n2 = m / 2;
       n2 -= n2 % 8;
-      if (lane == 0) {
-        S.stk[3 * sp + 2] = 1;                // revisit after both children
-        S.stk[3 * sp + 3] = o + n2;           // right
-        S.stk[3 * sp + 4] = m - n2;
-        S.stk[3 * sp + 5] = 0;
-        S.stk[3 * sp + 6] = o;                // left (popped first)
-        S.stk[3 * sp + 7] = n2;
-        S.stk[3 * sp + 8] = 0;
-      }
-      sp += 3;
+      S.stk[sp + 1] = 1;  // revisit after both children
+      S.stk[sp + 2] = m - n2;
+      S.stk[sp + 3] = 0;
+      S.stk[sp + 4] = n2;
+      S.stk[sp + 5] = 0;
+      sp += 6;
     } else {
-      wsync();
-      double b2 = S.vstk[vsp - 1], a2 = S.vstk[vsp - 2];
-      wsync();
-      if (lane == 0) S.vstk[vsp - 2] = a2 + b2;
-      vsp--;
+      const double b = vs[--vsp];
+      const double a = vs[--vsp];
+      vs[vsp++] = a + b;
     }
+  }
+  return vs[0];
+}
+
+template <class F>
+__device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
+  const int lane = lane_id();
+  int nl = 1;
+  if (n > 128) {
+    if (lane == 0) S.stk[191] = pw_plan(n, S);
+    wsync();
+    nl = S.stk[191];
+  }
+  const int j = lane & 7;
+  for (int b = 0; b < nl; b += 8) {  // accumulator chains, 8 leaves per pass
+    const int l = b + (lane >> 3);
+    if (l < nl) {
+      const int o = nl == 1 ? 0 : S.lo[l], m = nl == 1 ? n : S.len[l];
+      const int full = m - (m % 8);
+      double r = 0.0;
+      if (m >= 8) {
+        r = f(o + j);
+        for (int i = o + j + 8; i < o + full; i += 8) r += f(i);
+      }
+      S.acc[l * 8 + j] = r;
+    }
+  }
+  wsync();
+  for (int l = lane; l < nl; l += 64) {  // leaf combine + sequential tail
+    const int o = nl == 1 ? 0 : S.lo[l], m = nl == 1 ? n : S.len[l];
+    const double *a = S.acc + l * 8;
+    double res;
+    int i0;
+    if (m < 8) {
+      res = 0.0;
+      i0 = o;
+    } else {
+      res = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+      i0 = o + m - (m % 8);
+    }
+    for (int i = i0; i < o + m; i++) res += f(i);
+    S.val[l] = res;
+  }
+  wsync();
+  if (nl > 1) {
+    if (lane == 0) S.val[nl] = pw_combine(n, S, nl);
     wsync();
   }
-  return S.vstk[0];
+  const double r = S.val[nl > 1 ? nl : 0];
+  wsync();
+  return r;
 }
 
 // ------------------------------------------- numpy scalar argsort (BF) ----
-// aquicksort_<float_tag> / aheapsort_ (npysort), run by ONE lane on LDS.
+// aquicksort_<float_tag> / aheapsort_ (npysort), run by ONE lane on LDS
+// arrays (index form of the pointer algorithm); stack arrays live in LDS.
 __device__ __forceinline__ bool fless(float a, float b) { return a < b || (b != b && a == a); }
 
 __device__ void aheapsort_lds(const float *v, uint16_t *tosort, int n) {
@@ -343,11 +359,9 @@ __device__ void aheapsort_lds(const float *v, uint16_t *tosort, int n) {
   }
 }
 
-__device__ void aquicksort_lds(const float *v, uint16_t *t, int num) {
-  // index-based restatement of the pointer algorithm
+__device__ __noinline__ void aquicksort_lds(const float *v, uint16_t *t, int num, int32_t *stack) {
+  int32_t *depth = stack + 128;
   int pl = 0, pr = num - 1;
-  int stack[64];
-  int depth[32];
   int sp = 0, dp = 0;
   int cdepth = 0;
   for (int u = num; u >>= 1;) cdepth++;
@@ -401,22 +415,25 @@ __device__ void aquicksort_lds(const float *v, uint16_t *t, int num) {
 }
 
 // --------------------------------------------------------- env kernel ----
-struct WaveLds {
-  double *cpu, *mem;       // f64[P] each
-  float *fcpu, *fmem;      // f32 copies (obs view) for the heuristics
-  float *fkey;             // BF keys
-  uint16_t *ord;           // BF visiting order (ascending argsort)
-  uint16_t *acts;          // heuristic actions [V]
-  uint32_t *list;          // compacted waiting VMs [V]
-  uint8_t *ccomp, *mcomp;  // compressed sizes (hundredths) [V]
-  PwScratch pw;
+// Per-wave LDS carve (offsets from EnvParams, computed by the host).
+struct Lds {
+  EnvHdr *hdr;             // the env's 256-B header (scalars, RNG streams)
+  double *cpu, *mem;       // f64[P] PM resources (the env state)
+  float *fcpu, *fmem;      // f32[P] observation view used by the heuristics
+  float *fkey;             // BF keys fcpu + fmem
+  uint8_t *tc, *tm;        // per-PM largest fitting size (hundredths), f32 semantics
+  uint16_t *ord;           // BF ascending argsort, then reversed into visiting order
+  uint64_t *bc, *bm;       // [101][NW] fit bitmaps by size (bit = visiting position)
+  int32_t *sortstk;        // introsort stacks
+  uint64_t *stage;         // 64 staged accepted-VM words
+  uint8_t *ccomp, *mcomp;  // compressed sizes of existing VMs [V]
+  PwLds pw;
 };
 
-struct Scal {  // per-env scalars (wave-uniform)
-  Pcg rng[4];
-  Pcg seqbase[2];
-  int64_t timestep, total_requests, served, suspend_action, place_action, dropped;
-  double total_cpu_req, total_mem_req, waiting_ratio, tcm, tmm;
+// Exact k/100 for k = 0..127 (np.around(., 2) values), per block.
+struct Tables {
+  double cent[128];
+  float fcent[128];
 };
 
 __device__ __forceinline__ int w_pl(uint32_t w) { return (int)(w & 0xFFFFu); }
@@ -426,190 +443,264 @@ __device__ __forceinline__ uint32_t w_make(int pl, int cc, int cm) {
   return (uint32_t)pl | ((uint32_t)cc << 16) | ((uint32_t)cm << 24);
 }
 
-__device__ __forceinline__ void load_scal(const EnvHdr *h, Scal &S) {
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    S.rng[k].s = U128{h->rng[k][0], h->rng[k][1]};
-    S.rng[k].inc = U128{h->rng[k][2], h->rng[k][3]};
+__device__ __forceinline__ Pcg ld_pcg(const EnvHdr *h, int k) {
+  Pcg r;
+  r.s = U128{h->rng[k][0], h->rng[k][1]};
+  r.inc = U128{h->rng[k][2], h->rng[k][3]};
+  return r;
+}
+__device__ __forceinline__ void st_pcg(EnvHdr *h, int k, const Pcg &r) {
+  if (lane_id() == 0) {
+    h->rng[k][0] = r.s.hi;
+    h->rng[k][1] = r.s.lo;
   }
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    S.seqbase[k].s = U128{h->seqbase[k][0], h->seqbase[k][1]};
-    S.seqbase[k].inc = S.rng[k].inc;
-  }
-  S.timestep = h->timestep;
-  S.total_requests = h->total_requests;
-  S.served = h->served;
-  S.suspend_action = h->suspend_action;
-  S.place_action = h->place_action;
-  S.dropped = h->dropped;
-  S.total_cpu_req = h->total_cpu_req;
-  S.total_mem_req = h->total_mem_req;
-  S.waiting_ratio = h->waiting_ratio;
-  S.tcm = h->tcm;
-  S.tmm = h->tmm;
 }
 
-__device__ __forceinline__ void store_scal(EnvHdr *h, const Scal &S, int lane) {
-  // lane-parallel store of the 256-B header
-  uint64_t w = 0;
-  int k = lane >> 2, q = lane & 3;
-  if (lane < 16) {
-    const Pcg &r = S.rng[lane >> 2];
-    w = q == 0 ? r.s.hi : q == 1 ? r.s.lo : q == 2 ? r.inc.hi : r.inc.lo;
-  } else if (lane < 20) {
-    const Pcg &r = S.seqbase[(lane - 16) >> 1];
-    w = ((lane - 16) & 1) ? r.s.lo : r.s.hi;
-  } else if (lane < 32) {
-    int f = lane - 20;
-    double d = 0.0;
-    switch (f) {
-      case 0: w = (uint64_t)S.timestep; break;
-      case 1: w = (uint64_t)S.total_requests; break;
-      case 2: w = (uint64_t)S.served; break;
-      case 3: w = (uint64_t)S.suspend_action; break;
-      case 4: w = (uint64_t)S.place_action; break;
-      case 5: w = (uint64_t)S.dropped; break;
-      case 6: d = S.total_cpu_req; w = __double_as_longlong(d); break;
-      case 7: d = S.total_mem_req; w = __double_as_longlong(d); break;
-      case 8: d = S.waiting_ratio; w = __double_as_longlong(d); break;
-      case 9: d = S.tcm; w = __double_as_longlong(d); break;
-      case 10: d = S.tmm; w = __double_as_longlong(d); break;
-      default: w = 0;
+// Largest k in [0, 100] with f + FC[k] <= 1 in f32 (monotone in k), or -1.
+__device__ __forceinline__ int fit_threshold(float f, const float *fc) {
+  if (!(f + fc[0] <= 1.0f)) return -1;
+  int lo = 0, hi = 101;
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (f + fc[mid] <= 1.0f) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// Rebuild the fit bitmaps: bit i of bc[k][w] is set iff the PM at visiting
+// position w*64+i accepts a VM of cpu size k/100 (f32 obs arithmetic).
+__device__ __forceinline__ void build_bitmaps(const EnvParams &p, const Lds &L, bool bf) {
+  const int lane = lane_id();
+  const int P = p.P, NW = p.NW;
+  for (int w = 0; w < NW; w++) {
+    int pos = w * 64 + lane;
+    int q = pos < P ? (bf ? (int)L.ord[pos] : pos) : 0;
+    int tcq = pos < P ? (int)L.tc[q] - 1 : -1;
+    int tmq = pos < P ? (int)L.tm[q] - 1 : -1;
+    uint64_t c0 = 0, c1 = 0, m0 = 0, m1 = 0;
+    for (int k = 0; k < 101; k++) {
+      uint64_t bcw = ballot(tcq >= k), bmw = ballot(tmq >= k);
+      if ((k & 63) == lane) {
+        if (k < 64) { c0 = bcw; m0 = bmw; } else { c1 = bcw; m1 = bmw; }
+      }
+    }
+    L.bc[lane * NW + w] = c0;
+    L.bm[lane * NW + w] = m0;
+    if (lane + 64 < 101) {
+      L.bc[(lane + 64) * NW + w] = c1;
+      L.bm[(lane + 64) * NW + w] = m1;
     }
   }
-  (void)k;
-  if (lane < 32) reinterpret_cast<uint64_t *>(h)[lane] = w;
+  wsync();
 }
 
-// Exact k/100 for k = 0..100 (np.around(., 2) values), built per block.
-struct Tables {
-  double cent[128];
-  float fcent[128];
-};
-
-// The heuristic act (firstfit.py:21-38 / bestfit.py:21-40) on the current
-// state's f32 observation view, exact w.r.t. the reference's sequential loop:
-//  - every waiting VM's first feasible PM in scan order is found lane-parallel;
-//  - the earliest VM (index order) with a feasible PM wins and is applied;
-//    VMs before it stay infeasible forever (loads only grow), VMs after it
-//    keep their choice unless it was the winner's PM (FF) / always rescan (BF,
-//    whose order depends on every key);
-//  - repeat until no pending VM has a feasible PM.
-// Output: acts[v] in LDS (stay = current placement).
-template <int VPT>
-__device__ void heuristic_act(const EnvParams &p, const WaveLds &L, const Tables &T,
-                              const uint32_t (&wa)[VPT], int policy) {
-  const int lane = lane_id();
-  const int P = p.P, V = p.V, WAIT = p.P;
-  for (int i = lane; i < P; i += 64) {
-    L.fcpu[i] = (float)L.cpu[i];
-    L.fmem[i] = (float)L.mem[i];
+// First visiting position accepting sizes (kc, km), or -1.
+__device__ __forceinline__ int bm_query(const Lds &L, int NW, int kc, int km) {
+  for (int w = 0; w < NW; w++) {
+    uint64_t m = L.bc[kc * NW + w] & L.bm[km * NW + w];
+    if (m) return w * 64 + __ffsll((unsigned long long)m) - 1;
   }
-  // compact the waiting VMs in index order; stays for everyone
-  int nW = 0;
+  return -1;
+}
+
+__device__ __forceinline__ void bf_sort(const EnvParams &p, const Lds &L) {
+  const int lane = lane_id();
+  const int P = p.P;
+  for (int i = lane; i < P; i += 64) L.fkey[i] = L.fcpu[i] + L.fmem[i];
+  wsync();
+  if (lane == 0) {
+    for (int i = 0; i < P; i++) L.ord[i] = (uint16_t)i;
+    aquicksort_lds(L.fkey, L.ord, P, L.sortstk);
+    // reverse in place: np.flip(argsort) = visiting order
+    for (int i = 0, j = P - 1; i < j; i++, j--) {
+      uint16_t x = L.ord[i];
+      L.ord[i] = L.ord[j];
+      L.ord[j] = x;
+    }
+  }
+  wsync();
+}
+
+// One VM placement event of the env (env.py:74-84 for a WAIT -> PM move):
+// _resource_valid in f64, then _place_vm. Returns validity (wave-uniform).
+__device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int q, int kc, int km) {
+  double cq = L.cpu[q], mq = L.mem[q];
+  double vc = T.cent[kc], vm = T.cent[km];
+  bool ok = (cq + vc <= 1) && (mq + vm <= 1);
+  wsync();
+  if (ok && lane_id() == 0) {
+    L.cpu[q] = cq + vc;
+    L.mem[q] = mq + vm;
+  }
+  wsync();
+  return ok;
+}
+
+// FirstFitAgent.act / BestFitAgent.act (firstfit.py:21-38, bestfit.py:21-40)
+// on the pre-step f32 observation, fused with the action phase of step().
+// Exact w.r.t. the reference's sequential loop because:
+//  - a waiting VM's choice is "first visiting position whose PM fits", answered
+//    in O(P/64) from per-size fit bitmaps; the earliest VM (index order) with a
+//    fit wins; VMs before it never fit again (loads only grow);
+//  - the heuristic's state (f32 view) and the env's state (f64) are disjoint,
+//    so applying each winner's env event as soon as it is decided equals
+//    deciding every action first and stepping afterwards (env.py:68-88).
+template <int VPT>
+__device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds &L, const Tables &T,
+                                   uint32_t (&wa)[VPT], int policy, int32_t *act_out,
+                                   uint8_t *valid_out) {
+  const int lane = lane_id();
+  const int P = p.P, V = p.V, WAIT = p.P, NW = p.NW;
+  const bool bf = policy == 1;
+  uint32_t pend = 0;
+#pragma unroll
+  for (int s = 0; s < VPT; s++)
+    if (s * 64 + lane < V && w_pl(wa[s]) == WAIT) pend |= 1u << s;
+  uint32_t won = 0, bad = 0;
+  int64_t n_place = 0;
+  if (ballot(pend != 0)) {
+    for (int i = lane; i < P; i += 64) {
+      float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
+      L.fcpu[i] = fcv;
+      L.fmem[i] = fmv;
+      L.tc[i] = (uint8_t)(fit_threshold(fcv, T.fcent) + 1);
+      L.tm[i] = (uint8_t)(fit_threshold(fmv, T.fcent) + 1);
+    }
+    wsync();
+    if (bf) bf_sort(p, L);
+    build_bitmaps(p, L, bf);
+    for (;;) {
+      int ws = -1, wl = 0, wpos = 0;
+#pragma unroll
+      for (int s = 0; s < VPT; s++) {
+        bool pd = (pend >> s) & 1u;
+        int pos = pd ? bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) : -1;
+        uint64_t m = ballot(pos >= 0);
+        if (ws < 0 && m) {
+          ws = s;
+          wl = __ffsll((unsigned long long)m) - 1;
+          wpos = __builtin_amdgcn_readlane(pos, wl);
+        }
+      }
+      if (ws < 0) break;
+      // everything up to and including the winner is decided
+#pragma unroll
+      for (int s = 0; s < VPT; s++)
+        if (s < ws || (s == ws && lane <= wl)) pend &= ~(1u << s);
+      uint32_t ww = 0;
+#pragma unroll
+      for (int s = 0; s < VPT; s++)
+        if (s == ws) ww = rdlane(wa[s], wl);
+      const int kc = w_cc(ww), km = w_cm(ww);
+      const int q = bf ? (int)L.ord[wpos] : wpos;
+      // env event, f64 (env.py:55-56, 58-64)
+      bool ok = env_place(L, T, q, kc, km);
+      n_place += ok;
+      if (lane == wl) {
+#pragma unroll
+        for (int s = 0; s < VPT; s++)
+          if (s == ws) {
+            won |= 1u << s;
+            if (ok) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)q;
+            else bad |= 1u << s;
+          }
+        if (act_out) act_out[ws * 64 + wl] = q;
+      }
+      // heuristic state update (f32): FF updates cpu only (firstfit.py:36)
+      if (lane == 0) {
+        float nc = L.fcpu[q] + T.fcent[kc];
+        L.fcpu[q] = nc;
+        L.tc[q] = (uint8_t)(fit_threshold(nc, T.fcent) + 1);
+        if (bf) {
+          float nm = L.fmem[q] + T.fcent[km];
+          L.fmem[q] = nm;
+          L.tm[q] = (uint8_t)(fit_threshold(nm, T.fcent) + 1);
+        }
+      }
+      wsync();
+      if (bf) {
+        bf_sort(p, L);
+        build_bitmaps(p, L, true);
+      } else {  // only PM q's bit changes, for sizes above its new threshold
+        const int t = (int)L.tc[q] - 1;
+        const int w = q >> 6;
+        const uint64_t bit = 1ull << (q & 63);
+        for (int k = lane; k < 101; k += 64) {
+          uint64_t x = L.bc[k * NW + w];
+          L.bc[k * NW + w] = (t >= k) ? (x | bit) : (x & ~bit);
+        }
+        wsync();
+      }
+    }
+  }
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     int v = s * 64 + lane;
-    bool in = v < V;
-    int pl = w_pl(wa[s]);
-    if (in) L.acts[v] = (uint16_t)pl;
-    uint64_t m = ballot(in && pl == WAIT);
-    if (in && pl == WAIT) L.list[nW + below(m, lane)] = (uint32_t)v | (wa[s] & 0xFFFF0000u);
-    nW += __popcll(m);
-  }
-  wsync();
-  if (nW == 0) return;
-  const bool bf = policy == 1;
-  // per-lane compacted entries j: idx = j*64 + lane
-  int pos[VPT];    // scan position (index into visiting order); P = none
-  int stat[VPT];   // 0 = needs scan, 1 = found, 2 = no fit, 3 = won
-  float fc[VPT], fm[VPT];
-#pragma unroll
-  for (int j = 0; j < VPT; j++) {
-    int idx = j * 64 + lane;
-    uint32_t ent = idx < nW ? L.list[idx] : 0u;
-    fc[j] = T.fcent[(ent >> 16) & 0xFF];
-    fm[j] = T.fcent[ent >> 24];
-    pos[j] = 0;
-    stat[j] = idx < nW ? 0 : 3;
-  }
-  if (bf) {
-    for (int i = lane; i < P; i += 64) L.fkey[i] = L.fcpu[i] + L.fmem[i];
-    wsync();
-    if (lane == 0) {
-      for (int i = 0; i < P; i++) L.ord[i] = (uint16_t)i;
-      aquicksort_lds(L.fkey, L.ord, P);
+    if (v < V) {
+      if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(wa[s]);
+      if (valid_out) valid_out[v] = (uint8_t)!((bad >> s) & 1u);
     }
-    wsync();
   }
-  for (;;) {
-    // scan pending entries from pos
+  return n_place;
+}
+
+// Action phase of step() for external actions (env.py:68-88): per slot of 64
+// VMs, the events (WAIT -> PM place attempts, PM -> WAIT suspends) are applied
+// in ascending VM order by a wave-uniform loop over the ballot.
+template <int VPT>
+__device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L, const Tables &T,
+                               uint32_t (&wa)[VPT], const int32_t *act_row, uint8_t *valid_out,
+                               int64_t &n_place, int64_t &n_susp) {
+  const int lane = lane_id();
+  const int P = p.P, V = p.V, WAIT = p.P;
 #pragma unroll
-    for (int j = 0; j < VPT; j++) {
-      if (stat[j] == 0) {
-        int i = pos[j];
-        for (; i < P; i++) {
-          int q = bf ? (int)L.ord[P - 1 - i] : i;
-          if (L.fcpu[q] + fc[j] <= 1.0f && L.fmem[q] + fm[j] <= 1.0f) break;
+  for (int s = 0; s < VPT; s++) {
+    const int v = s * 64 + lane;
+    const bool in = v < V;
+    const int c = w_pl(wa[s]);
+    const int t = in ? act_row[v] : c;
+    const bool isplace = in && c == WAIT && t >= 0 && t < P;
+    const bool issusp = in && c < P && t == WAIT;
+    uint64_t evm = ballot(isplace || issusp);
+    uint64_t okm = 0;
+    const uint32_t me = wa[s];
+    while (evm) {  // wave-uniform, ascending lane = ascending VM index
+      const int l = __ffsll((unsigned long long)evm) - 1;
+      evm &= evm - 1;
+      const uint32_t ew = rdlane(me, l);
+      const int et = __builtin_amdgcn_readlane(t, l);
+      const int ec = w_pl(ew);
+      const double vc = T.cent[w_cc(ew)], vm = T.cent[w_cm(ew)];
+      const int q = (ec == WAIT) ? et : ec;
+      double cq = L.cpu[q], mq = L.mem[q];
+      bool eok = true;
+      if (ec == WAIT) {
+        eok = (cq + vc <= 1) && (mq + vm <= 1);
+        if (eok) {
+          cq = cq + vc;
+          mq = mq + vm;
         }
-        pos[j] = i;
-        stat[j] = i < P ? 1 : 2;
+      } else {
+        cq = cq - vc;
+        mq = mq - vm;
       }
-    }
-    // earliest found entry
-    int wj = -1, wl = 0;
-#pragma unroll
-    for (int j = 0; j < VPT; j++) {
-      uint64_t m = ballot(stat[j] == 1);
-      if (wj < 0 && m) {
-        wj = j;
-        wl = __ffsll((unsigned long long)m) - 1;
-      }
-    }
-    if (wj < 0) break;
-    // winner data to every lane
-    int wpos = 0, widx = wj * 64 + wl;
-    float wfc = 0.f, wfm = 0.f;
-#pragma unroll
-    for (int j = 0; j < VPT; j++)
-      if (j == wj) {
-        wpos = __shfl(pos[j], wl);
-        wfc = __shfl(fc[j], wl);
-        wfm = __shfl(fm[j], wl);
-      }
-    int q = bf ? (int)L.ord[P - 1 - wpos] : wpos;
-    uint32_t went = L.list[widx];
-    wsync();
-    if (lane == 0) {
-      L.acts[went & 0xFFFF] = (uint16_t)q;
-      L.fcpu[q] = L.fcpu[q] + wfc;
-      if (bf) L.fmem[q] = L.fmem[q] + wfm;  // FF leaves memory stale (firstfit.py:36)
-    }
-    wsync();
-#pragma unroll
-    for (int j = 0; j < VPT; j++) {
-      int idx = j * 64 + lane;
-      if (idx == widx) stat[j] = 3;
-      else if (stat[j] == 1 && idx > widx) {
-        if (bf)
-          { stat[j] = 0; pos[j] = 0; }
-        else if (pos[j] == q)
-          stat[j] = 0;  // rescan from the winner's PM on
-      }
-    }
-    if (bf) {
-      for (int i = lane; i < P; i += 64) L.fkey[i] = L.fcpu[i] + L.fmem[i];
       wsync();
       if (lane == 0) {
-        for (int i = 0; i < P; i++) L.ord[i] = (uint16_t)i;
-        aquicksort_lds(L.fkey, L.ord, P);
+        L.cpu[q] = cq;
+        L.mem[q] = mq;
       }
+      okm |= (uint64_t)eok << l;
       wsync();
     }
+    bool ok = (t == c) || issusp;
+    if (isplace) ok = (okm >> lane) & 1ull;
+    n_place += __popcll(okm & ballot(isplace));
+    n_susp += __popcll(ballot(issusp));
+    if (ok && t != c && in) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)t;
+    if (valid_out && in) valid_out[v] = (uint8_t)ok;
   }
-  wsync();
 }
+
 
 // kl_divergence (env.py:8-17) in numpy/LAPACK/OpenBLAS evaluation order.
 __device__ __forceinline__ double kl_reward(double tcm, double tmm, double tcv, double tmv,
@@ -624,219 +715,191 @@ __device__ __forceinline__ double kl_reward(double tcm, double tmm, double tcv, 
   return -kl;
 }
 
-// One VmEnv.step (env.py:66-103) on the wave's env. act_row: external
-// actions (global) or null (use L.acts from heuristic_act).
+// kl reward branch (env.py:124-149), out of line: it runs only for
+// reward_function == "kl" and is register-heavy (six reductions, log/exp).
+__device__ __forceinline__ double kl_block(const double *cpu, const double *mem, int P,
+                                        const uint8_t *ccp, const uint8_t *cmp,
+                                        const double *cent, int n_ex, double sum_c,
+                                        double sum_m, double tcm, double tmm, PwLds S) {
+  const double cm_ = wave_pw_sum(P, [=](int i) { return cpu[i]; }, S) / (double)P;
+  const double mm_ = wave_pw_sum(P, [=](int i) { return mem[i]; }, S) / (double)P;
+  double cv = wave_pw_sum(P, [=](int i) { double d = cpu[i] - cm_; return d * d; }, S) /
+              (double)P;
+  double mv = wave_pw_sum(P, [=](int i) { double d = mem[i] - mm_; return d * d; }, S) /
+              (double)P;
+  if (cv == 0) cv = 1e-6;
+  if (mv == 0) mv = 1e-6;
+  const double mc = sum_c / (double)n_ex, mmv = sum_m / (double)n_ex;
+  double tcv = wave_pw_sum(n_ex, [=](int i) { double d = cent[ccp[i]] - mc; return d * d; }, S) /
+               (double)n_ex;
+  double tmv = wave_pw_sum(n_ex, [=](int i) { double d = cent[cmp[i]] - mmv; return d * d; }, S) /
+               (double)n_ex;
+  if (tcv == 0) tcv = 1e-6;
+  if (tmv == 0) tmv = 1e-6;
+  return (tcm == 0 || tmm == 0) ? 0.0 : kl_reward(tcm, tmm, tcv, tmv, cm_, mm_, cv, mv);
+}
+
+// Everything of step() after the action phase: _run_vms, _accept_vm_requests,
+// stats + reward, termination (env.py:101, 108-163, 244-293).
 template <int VPT>
-__device__ double env_step(const EnvParams &p, const WaveLds &L, const Tables &T, Scal &S,
-                           uint32_t (&wa)[VPT], uint32_t (&rem)[VPT], const int32_t *act_row,
-                           uint8_t *valid_row, int32_t *act_out_row, bool &terminated) {
+__device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, const Tables &T,
+                           uint32_t (&wa)[VPT], uint32_t (&rem)[VPT], bool &terminated) {
   const int lane = lane_id();
   const int P = p.P, V = p.V, WAIT = p.P, NUL = p.P + 1;
-  // ---- 1. per-VM validation + apply, VM order (env.py:68-88) ------------
-  int64_t n_place = 0, n_susp = 0;
-#pragma unroll
-  for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
-    bool in = v < V;
-    int c = w_pl(wa[s]);
-    int t = c;
-    if (in) t = act_row ? act_row[v] : (int)L.acts[v];
-    if (act_out_row && in) act_out_row[v] = t;
-    bool isplace = in && c == WAIT && t >= 0 && t < P;
-    bool issusp = in && c < P && t == WAIT;
-    bool ok = (t == c) || issusp;
-    uint64_t evm = ballot(isplace || issusp);
-    uint64_t okm = 0;
-    uint32_t me = wa[s];
-    while (evm) {  // wave-uniform, ascending lane = ascending VM index
-      int l = __ffsll((unsigned long long)evm) - 1;
-      evm &= evm - 1;
-      uint32_t ew = rdlane(me, l);
-      int et = __builtin_amdgcn_readlane(t, l);
-      int ec = w_pl(ew);
-      double vc = T.cent[w_cc(ew)], vm = T.cent[w_cm(ew)];
-      int q = (ec == WAIT) ? et : ec;
-      double cq = L.cpu[q], mq = L.mem[q];
-      bool eok = true;
-      if (ec == WAIT) {  // place: _resource_valid (env.py:55-56), then _place_vm
-        eok = (cq + vc <= 1) && (mq + vm <= 1);
-        if (eok) {
-          cq = cq + vc;
-          mq = mq + vm;
-        }
-      } else {  // suspend: _free_pm
-        cq = cq - vc;
-        mq = mq - vm;
-      }
-      if (lane == 0) {
-        L.cpu[q] = cq;
-        L.mem[q] = mq;
-      }
-      okm |= (uint64_t)eok << l;
-      wsync();
-    }
-    if (isplace) ok = (okm >> lane) & 1ull;
-    n_place += __popcll(okm & ballot(isplace));
-    n_susp += __popcll(ballot(issusp));
-    if (ok && t != c && in) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)t;
-    if (valid_row && in) valid_row[v] = (uint8_t)ok;
-  }
-  S.place_action += n_place;
-  S.suspend_action += n_susp;
-  // ---- 2. _run_vms (env.py:244-268) --------------------------------------
+  EnvHdr *H = L.hdr;
+  // ---- _run_vms (env.py:244-268) ----
   int64_t n_term = 0;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
-    bool in = v < V;
-    int c = w_pl(wa[s]);
-    bool running = in && c < P;
+    const bool in = s * 64 + lane < V;
+    const bool running = in && w_pl(wa[s]) < P;
     if (running && rem[s] > 0) rem[s] -= 1;
-    bool term = running && rem[s] == 0;
-    uint64_t tm = ballot(term);
-    uint32_t me = wa[s];
-    uint64_t it = tm;
-    while (it) {
-      int l = __ffsll((unsigned long long)it) - 1;
+    const bool term = running && rem[s] == 0;
+    uint64_t it = ballot(term);
+    n_term += __popcll(it);
+    const uint32_t me = wa[s];
+    while (it) {  // frees in ascending VM order (env.py:260-262)
+      const int l = __ffsll((unsigned long long)it) - 1;
       it &= it - 1;
-      uint32_t ew = rdlane(me, l);
-      int q = w_pl(ew);
-      double cq = L.cpu[q] - T.cent[w_cc(ew)];
-      double mq = L.mem[q] - T.cent[w_cm(ew)];
+      const uint32_t ew = rdlane(me, l);
+      const int q = w_pl(ew);
+      const double cq = L.cpu[q] - T.cent[w_cc(ew)];
+      const double mq = L.mem[q] - T.cent[w_cm(ew)];
+      wsync();
       if (lane == 0) {
         L.cpu[q] = cq;
         L.mem[q] = mq;
       }
       wsync();
     }
-    n_term += __popcll(tm);
     if (term) {
       wa[s] = w_make(NUL, 0, 0);
       rem[s] = 0;
     }
   }
-  S.served += n_term;
   for (int i = lane; i < P; i += 64) {  // precision clamp (env.py:267-268)
     if (L.cpu[i] < 1e-7) L.cpu[i] = 0;
     if (L.mem[i] < 1e-7) L.mem[i] = 0;
   }
-  wsync();
-  // ---- 3. _accept_vm_requests (env.py:271-293) ---------------------------
-  int64_t arrivals = poisson(S.rng[2], p.arr);
-  S.total_requests += arrivals;
+  // ---- _accept_vm_requests (env.py:271-293) ----
+  const int64_t arrivals = poisson_lds(H->rng[2], p.pois + 0);
   int n_null = 0;
 #pragma unroll
-  for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
-    n_null += __popcll(ballot(v < V && w_pl(wa[s]) == NUL));
-  }
-  int64_t k = arrivals < n_null ? arrivals : n_null;
+  for (int s = 0; s < VPT; s++)
+    n_null += __popcll(ballot(s * 64 + lane < V && w_pl(wa[s]) == NUL));
+  const int64_t k = arrivals < n_null ? arrivals : n_null;
+  wsync();
   if (k > 0) {
+    // ranks of the NULL slots in ascending VM order (to_accept, env.py:276-277)
+    int rk[VPT];
     int base = 0;
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
-      int v = s * 64 + lane;
-      bool isnull = v < V && w_pl(wa[s]) == NUL;
-      uint64_t nm = ballot(isnull);
-      int r = base + below(nm, lane);
-      uint64_t am = ballot(isnull && r < k);
-      while (am) {  // ascending slot order (rng4 draws in to_accept order)
-        int l = __ffsll((unsigned long long)am) - 1;
-        am &= am - 1;
-        int cc = (int)rint((p.seq_lo + p.seq_range * next_double(S.rng[0])) * 100.0);
-        int cm = (int)rint((p.seq_lo + p.seq_range * next_double(S.rng[1])) * 100.0);
-        uint32_t rr = (uint32_t)(poisson(S.rng[3], p.svc) + 1);
-        if (lane == l) {
-          wa[s] = w_make(WAIT, cc, cm);
-          rem[s] = rr;
-          L.ccomp[r] = (uint8_t)cc;
-          L.mcomp[r] = (uint8_t)cm;
-        }
-      }
+      const bool isnull = s * 64 + lane < V && w_pl(wa[s]) == NUL;
+      const uint64_t nm = ballot(isnull);
+      rk[s] = isnull ? base + below(nm, lane) : -1;
       base += __popcll(nm);
     }
-    wsync();
-    const uint8_t *cc = L.ccomp, *cm = L.mcomp;
+    // draws in to_accept order, 64 per chunk: sizes from rng1/rng2 (the popped
+    // sequences, env.py:279-287) and planned runtimes from rng4 (env.py:289)
+    for (int c0 = 0; c0 < k; c0 += 64) {
+      const int cn = (int)(k - c0 < 64 ? k - c0 : 64);
+      Pcg r1 = ld_pcg(H, 0), r2 = ld_pcg(H, 1);
+      for (int j = 0; j < cn; j++) {
+        const int cc = (int)rint((p.seq_lo + p.seq_range * next_double(r1)) * 100.0);
+        const int cm = (int)rint((p.seq_lo + p.seq_range * next_double(r2)) * 100.0);
+        const uint32_t rr = (uint32_t)(poisson_lds(H->rng[3], p.pois + 1) + 1);
+        if (lane == 0) {
+          L.stage[j] = (uint64_t)w_make(WAIT, cc, cm) | ((uint64_t)rr << 32);
+          L.ccomp[c0 + j] = (uint8_t)cc;
+          L.mcomp[c0 + j] = (uint8_t)cm;
+        }
+      }
+      st_pcg(H, 0, r1);
+      st_pcg(H, 1, r2);
+      wsync();
+#pragma unroll
+      for (int s = 0; s < VPT; s++) {
+        if (rk[s] >= c0 && rk[s] < c0 + cn) {
+          const uint64_t w = L.stage[rk[s] - c0];
+          wa[s] = (uint32_t)w;
+          rem[s] = (uint32_t)(w >> 32);
+        }
+      }
+      wsync();
+    }
+    const uint8_t *ccp = L.ccomp, *cmp = L.mcomp;
     const double *cent = T.cent;
-    S.total_cpu_req += wave_pw_sum((int)k, [&](int i) { return cent[cc[i]]; }, L.pw);
-    S.total_mem_req += wave_pw_sum((int)k, [&](int i) { return cent[cm[i]]; }, L.pw);
-    wsync();
+    const double sc = wave_pw_sum((int)k, [=](int i) { return cent[ccp[i]]; }, L.pw);
+    const double sm = wave_pw_sum((int)k, [=](int i) { return cent[cmp[i]]; }, L.pw);
+    if (lane == 0) {
+      H->total_cpu_req = H->total_cpu_req + sc;
+      H->total_mem_req = H->total_mem_req + sm;
+    }
   }
-  S.dropped += arrivals - k;
-  // ---- 4. stats + reward (env.py:112-156) --------------------------------
+  // ---- stats + reward (env.py:112-156) ----
   int n_ex = 0, n_w = 0;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
-    bool in = v < V;
-    int c = w_pl(wa[s]);
-    uint64_t em = ballot(in && c <= WAIT);
+    const bool in = s * 64 + lane < V;
+    const int c = w_pl(wa[s]);
+    const uint64_t em = ballot(in && c <= WAIT);
     if (in && c <= WAIT) {
-      int r = n_ex + below(em, lane);
-      L.ccomp[r] = (uint8_t)w_cc(wa[s]);
-      L.mcomp[r] = (uint8_t)w_cm(wa[s]);
+      const int rk = n_ex + below(em, lane);
+      L.ccomp[rk] = (uint8_t)w_cc(wa[s]);
+      L.mcomp[rk] = (uint8_t)w_cm(wa[s]);
     }
     n_ex += __popcll(em);
     n_w += __popcll(ballot(in && c == WAIT));
   }
   wsync();
-  S.waiting_ratio = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
+  const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
   const uint8_t *ccp = L.ccomp, *cmp = L.mcomp;
   const double *cent = T.cent;
-  auto fx = [&](int i) { return cent[ccp[i]]; };
-  auto fy = [&](int i) { return cent[cmp[i]]; };
-  double sum_c = wave_pw_sum(n_ex, fx, L.pw);
-  double sum_m = wave_pw_sum(n_ex, fy, L.pw);
-  S.tcm = sum_c / (double)P;
-  if (p.cap_target_util && S.tcm > 1) S.tcm = 1.0;
-  S.tmm = sum_m / (double)P;
-  if (p.cap_target_util && S.tmm > 1) S.tmm = 1.0;
+  const double sum_c = wave_pw_sum(n_ex, [=](int i) { return cent[ccp[i]]; }, L.pw);
+  const double sum_m = wave_pw_sum(n_ex, [=](int i) { return cent[cmp[i]]; }, L.pw);
+  double tcm = sum_c / (double)P;
+  if (p.cap_target_util && tcm > 1) tcm = 1.0;
+  double tmm = sum_m / (double)P;
+  if (p.cap_target_util && tmm > 1) tmm = 1.0;
   double reward = 0.0;
   if (n_ex > 0) {
     const double *cpu = L.cpu, *mem = L.mem;
     if (p.reward == 2) {  // kl
-      double cm_ = wave_pw_sum(P, [&](int i) { return cpu[i]; }, L.pw) / (double)P;
-      double mm_ = wave_pw_sum(P, [&](int i) { return mem[i]; }, L.pw) / (double)P;
-      double cv = wave_pw_sum(P, [&](int i) { double d = cpu[i] - cm_; return d * d; }, L.pw) /
-                  (double)P;
-      double mv = wave_pw_sum(P, [&](int i) { double d = mem[i] - mm_; return d * d; }, L.pw) /
-                  (double)P;
-      if (cv == 0) cv = 1e-6;
-      if (mv == 0) mv = 1e-6;
-      double mc = sum_c / (double)n_ex, mmv = sum_m / (double)n_ex;
-      double tcv = wave_pw_sum(n_ex, [&](int i) { double d = cent[ccp[i]] - mc; return d * d; },
-                               L.pw) / (double)n_ex;
-      double tmv = wave_pw_sum(n_ex, [&](int i) { double d = cent[cmp[i]] - mmv; return d * d; },
-                               L.pw) / (double)n_ex;
-      if (tcv == 0) tcv = 1e-6;
-      if (tmv == 0) tmv = 1e-6;
-      if (S.tcm == 0 || S.tmm == 0)
-        reward = 0.0;
-      else
-        reward = kl_reward(S.tcm, S.tmm, tcv, tmv, cm_, mm_, cv, mv);
+      reward = kl_block(cpu, mem, P, ccp, cmp, cent, n_ex, sum_c, sum_m, tcm, tmm, L.pw);
     } else if (p.reward == 1) {  // ut
-      double sc = wave_pw_sum(P, [&](int i) { return cpu[i]; }, L.pw);
-      double sm = wave_pw_sum(P, [&](int i) { return mem[i]; }, L.pw);
+      const double sc = wave_pw_sum(P, [=](int i) { return cpu[i]; }, L.pw);
+      const double sm = wave_pw_sum(P, [=](int i) { return mem[i]; }, L.pw);
       reward = p.beta * sc + (1 - p.beta) * sm;
     } else {  // wr
-      reward = -S.waiting_ratio;
+      reward = -wr;
     }
   }
+  // ---- counters, termination (env.py:160-163, 101) ----
+  const int64_t ts = H->timestep;
+  terminated = ts >= p.limit;
   wsync();
-  // ---- 5. termination (env.py:160-163, 101) ------------------------------
-  terminated = S.timestep >= p.limit;
-  S.timestep += 1;
+  if (lane == 0) {
+    H->timestep = ts + 1;
+    H->total_requests += arrivals;
+    H->served += n_term;
+    H->dropped += arrivals - k;
+    H->waiting_ratio = wr;
+    H->tcm = tcm;
+    H->tmm = tmm;
+  }
+  wsync();
   return reward;
 }
 
 template <int VPT>
-__device__ void write_obs(const EnvParams &p, const WaveLds &L, const Tables &T,
+__device__ __forceinline__ void write_obs(const EnvParams &p, const Lds &L, const Tables &T,
                           const uint32_t (&wa)[VPT], float *obs) {
   const int lane = lane_id();
   const int V = p.V, P = p.P;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
+    const int v = s * 64 + lane;
     if (v < V) {
       obs[v] = (float)w_pl(wa[s]);
       obs[V + v] = T.fcent[w_cc(wa[s])];
@@ -851,39 +914,37 @@ __device__ void write_obs(const EnvParams &p, const WaveLds &L, const Tables &T,
 
 // get_invalid_action_mask(masked=True) (env.py:45-53), bit-packed, 1 = invalid.
 template <int VPT>
-__device__ void write_mask(const EnvParams &p, const WaveLds &L, const Tables &T,
+__device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, const Tables &T,
                            const uint32_t (&wa)[VPT], uint32_t *bits) {
   const int lane = lane_id();
   const int V = p.V, P = p.P, A = p.A, W = p.W32, WAIT = p.P, NUL = p.P + 1;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
-    bool in = v < V;
-    int c = in ? w_pl(wa[s]) : NUL;
-    double vc = T.cent[w_cc(wa[s])], vm = T.cent[w_cm(wa[s])];
-    bool waiting = in && c == WAIT;
-    bool anyw = ballot(waiting) != 0;
+    const int v = s * 64 + lane;
+    const bool in = v < V;
+    const int c = in ? w_pl(wa[s]) : NUL;
+    const double vc = T.cent[w_cc(wa[s])], vm = T.cent[w_cm(wa[s])];
+    const bool waiting = in && c == WAIT;
+    const bool anyw = ballot(waiting) != 0;
     for (int w = 0; w < W; w++) {
-      uint32_t word = 0xFFFFFFFFu;  // all invalid
-      int a0 = w * 32;
-      // statically valid entries: stay, and running -> WAIT
-      if (c >= a0 && c < a0 + 32 && c < A) word &= ~(1u << (c - a0));
-      if (c < P && WAIT >= a0 && WAIT < a0 + 32) word &= ~(1u << (WAIT - a0));
+      uint32_t word = 0xFFFFFFFFu;
+      const int a0 = w * 32;
+      if (c >= a0 && c < a0 + 32 && c < A) word &= ~(1u << (c - a0));  // stay
+      if (c < P && WAIT >= a0 && WAIT < a0 + 32) word &= ~(1u << (WAIT - a0));  // suspend
       if (anyw) {
-        int hi = min(a0 + 32, P);
+        const int hi = min(a0 + 32, P);
         for (int q = a0; q < hi; q++) {  // uniform q: LDS broadcast reads
-          bool fit = (L.cpu[q] + vc <= 1) && (L.mem[q] + vm <= 1);
+          const bool fit = (L.cpu[q] + vc <= 1) && (L.mem[q] + vm <= 1);
           if (waiting && fit) word &= ~(1u << (q - a0));
         }
       }
-      // bits beyond A stay set (never valid)
       if (in) bits[(int64_t)v * W + w] = word;
     }
   }
 }
 
 template <int VPT>
-__global__ __launch_bounds__(256) void k_env(EnvParams p, StepOut o) {
+__global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
   extern __shared__ __align__(16) char lds[];
   __shared__ Tables T;
   for (int i = threadIdx.x; i < 128; i += blockDim.x) {
@@ -896,60 +957,72 @@ __global__ __launch_bounds__(256) void k_env(EnvParams p, StepOut o) {
   const int e = uni(blockIdx.x * kWavesPerBlock + wid);
   if (e >= p.N) return;
   char *base = lds + wid * p.lds_wave_bytes;
-  WaveLds L;
+  Lds L;
+  L.hdr = reinterpret_cast<EnvHdr *>(base + p.off_hdr);
   L.cpu = reinterpret_cast<double *>(base + p.off_pm);
   L.mem = L.cpu + p.P;
   L.fcpu = reinterpret_cast<float *>(base + p.off_fpm);
   L.fmem = L.fcpu + p.P;
   L.fkey = L.fmem + p.P;
+  L.tc = reinterpret_cast<uint8_t *>(base + p.off_thr);
+  L.tm = L.tc + p.P;
   L.ord = reinterpret_cast<uint16_t *>(base + p.off_ord);
-  L.acts = L.ord + p.P;
-  L.list = reinterpret_cast<uint32_t *>(base + p.off_list);
+  L.bc = reinterpret_cast<uint64_t *>(base + p.off_bits);
+  L.bm = L.bc + 101 * p.NW;
+  L.sortstk = reinterpret_cast<int32_t *>(base + p.off_sort);
+  L.stage = reinterpret_cast<uint64_t *>(base + p.off_stage);
   L.ccomp = reinterpret_cast<uint8_t *>(base + p.off_ccomp);
-  L.mcomp = reinterpret_cast<uint8_t *>(base + p.off_mcomp);
-  {
-    int32_t *lf = reinterpret_cast<int32_t *>(base + p.off_leaf);
-    int nl = (p.V + 63) / 64 + 8;
-    L.pw.lo = lf;
-    L.pw.len = lf + nl;
-    L.pw.stk = lf + 2 * nl;
-    L.pw.val = reinterpret_cast<double *>(base + p.off_tmp);
-    L.pw.vstk = L.pw.val + nl;
-  }
+  L.mcomp = L.ccomp + p.V;
+  L.pw.lo = reinterpret_cast<int32_t *>(base + p.off_leaf);
+  L.pw.len = L.pw.lo + p.n_leaf;
+  L.pw.stk = L.pw.len + p.n_leaf;
+  L.pw.acc = reinterpret_cast<double *>(base + p.off_leafval);
+  L.pw.val = L.pw.acc + 8 * p.n_leaf;
   const int V = p.V, P = p.P;
+  // ---- load: VM words to registers, PM resources + header to LDS ----
   const uint64_t *vmw = p.vmw + (int64_t)e * V;
-  const double *pm = p.pm + (int64_t)e * 2 * P;
-  // ---- load state: VM words to registers, PM resources to LDS ----
   uint32_t wa[VPT], rem[VPT];
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
-    uint64_t w = v < V ? vmw[v] : (uint64_t)(P + 1);
+    const int v = s * 64 + lane;
+    const uint64_t w = v < V ? vmw[v] : (uint64_t)(P + 1);
     wa[s] = (uint32_t)w;
     rem[s] = (uint32_t)(w >> 32);
   }
+  const double *pm = p.pm + (int64_t)e * 2 * P;
   for (int i = lane; i < 2 * P; i += 64) L.cpu[i] = pm[i];
-  Scal S;
-  load_scal(p.hdr + e, S);
+  if (lane < 32)
+    reinterpret_cast<uint64_t *>(L.hdr)[lane] = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane];
   wsync();
   bool term = false;
   int64_t ndone = 0;
   for (int k = 0; k < o.k_steps; k++) {
     const bool last = k == o.k_steps - 1;
-    const int32_t *act_row = nullptr;
+    uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
+    int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
+    int64_t n_place = 0, n_susp = 0;
     if (o.policy >= 0)
-      heuristic_act<VPT>(p, L, T, wa, o.policy);
+      n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row);
     else
-      act_row = o.actions + (int64_t)e * V;
-    double r = env_step<VPT>(p, L, T, S, wa, rem, act_row,
-                             (last && o.valid) ? o.valid + (int64_t)e * V : nullptr,
-                             (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr, term);
+      external_apply<VPT>(p, L, T, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
+    wsync();
+    if (lane == 0) {
+      L.hdr->place_action += n_place;
+      L.hdr->suspend_action += n_susp;
+    }
+    wsync();
+    const double r = env_tail<VPT>(p, L, T, wa, rem, term);
     if (o.reward && lane == 0) o.reward[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
-  if (o.k_steps == 0 && o.policy >= 0 && o.act_out) {  // act only (no step)
-    heuristic_act<VPT>(p, L, T, wa, o.policy);
-    for (int v = lane; v < V; v += 64) o.act_out[(int64_t)e * V + v] = L.acts[v];
+  if (o.k_steps == 0 && o.policy >= 0 && o.act_out) {
+    // act only: decide on a scratch copy, the state is not stored
+    uint32_t wt[VPT];
+#pragma unroll
+    for (int s = 0; s < VPT; s++) wt[s] = wa[s];
+    heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr);
+    for (int i = lane; i < 2 * P; i += 64) L.cpu[i] = pm[i];  // undo env events
+    wsync();
   }
   if (o.obs) write_obs<VPT>(p, L, T, wa, o.obs + (int64_t)e * p.D);
   if (o.mask_bits) write_mask<VPT>(p, L, T, wa, o.mask_bits + (int64_t)e * V * p.W32);
@@ -959,12 +1032,13 @@ __global__ __launch_bounds__(256) void k_env(EnvParams p, StepOut o) {
     uint64_t *vmo = p.vmw + (int64_t)e * V;
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
-      int v = s * 64 + lane;
+      const int v = s * 64 + lane;
       if (v < V) vmo[v] = (uint64_t)wa[s] | ((uint64_t)rem[s] << 32);
     }
     double *pmo = p.pm + (int64_t)e * 2 * P;
     for (int i = lane; i < 2 * P; i += 64) pmo[i] = L.cpu[i];
-    store_scal(p.hdr + e, S, lane);
+    if (lane < 32)
+      reinterpret_cast<uint64_t *>(p.hdr + e)[lane] = reinterpret_cast<uint64_t *>(L.hdr)[lane];
   }
 }
 

@@ -52,12 +52,16 @@ struct EnvParams {
   int64_t M2;             // 2 * max(training_steps, eval_steps)
   double beta, seq_lo, seq_range;
   PoisConst arr, svc;     // arrivals (rng3), service lengths (rng4)
+  const PoisConst *pois;  // device copy: [0] arrivals, [1] service lengths
   uint64_t *vmw;
   double *pm;
   EnvHdr *hdr;
   // per-wave LDS carve (bytes); offsets inside one wave's region
   int32_t lds_wave_bytes;
-  int32_t off_pm, off_fpm, off_ord, off_list, off_ccomp, off_mcomp, off_tmp, off_leaf;
+  int32_t NW;      // ceil(P/64) words per fit bitmap row
+  int32_t n_leaf;  // capacity of the pairwise-sum leaf list
+  int32_t off_hdr, off_pm, off_fpm, off_thr, off_ord, off_bits, off_sort, off_ccomp;
+  int32_t off_leaf, off_leafval, off_stage;
 };
 
 struct StepOut {

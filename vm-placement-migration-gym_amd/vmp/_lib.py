@@ -5,7 +5,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvmp.so")
+LIB_PATH = os.environ.get("VMP_LIB_PATH") or os.path.join(_HERE, "libvmp.so")
 
 REWARDS = {"wr": 0, "ut": 1, "kl": 2}
 SEQUENCES = {"uniform": 0, "lowuniform": 1, "highuniform": 2}
