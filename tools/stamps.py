@@ -1,0 +1,46 @@
+"""Phase breakdown of the env kernel from a -DVMP_STAMPS build (diagnostic).
+Usage: VMP_LIB_PATH=.../libvmp_stamps.so python tools/stamps.py [envs] [vms]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "vm-placement-migration-gym_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from vmp import _lib  # noqa: E402
+from vmp.batched import BatchedVmEnv  # noqa: E402
+from vmp.config import Config  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+V = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
+cfg = Config(pms=100, vms=V, arrival_rate=1.8182, service_length=1000, training_steps=10000,
+             eval_steps=100000, seed=0, reward_function="wr", allow_null_action=True)
+env = BatchedVmEnv(cfg, N)
+env.eval(True)
+for _ in range(25):
+    env.rollout("firstfit", 100)
+buf = torch.zeros((N, 16), dtype=torch.int64, device="cuda")
+_lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
+K = 50
+for _ in range(K):
+    env.heuristic_step("firstfit")
+torch.cuda.synchronize()
+_lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
+torch.cuda.synchronize()
+st = buf.cpu().numpy().astype(np.float64) / K
+names = ["loop-end", "act+apply(rest)", "run_vms", "accept", "stats(rest)+reward", "obs", "store",
+         "-", "heur:prep", "heur:bitmaps", "heur:resolve", "stats:compress", "stats:pw-sums",
+         "pro:start->hdr/pm loaded", "pro:predraw", "pro:VM words loaded"]
+tot = st[:, :16].sum(1) - st[:, 7] - st[:, 9]
+print(f"N={N} V={V}: mean cycles per env-step (per wave) = {tot.mean():.0f}")
+for i in range(16):
+    if names[i] != "-" and i not in (7, 9):
+        print(f"  {names[i]:20s} {st[:, i].mean():10.0f}  ({100 * st[:, i].mean() / tot.mean():5.1f}%)")
+ctr = env.counters().cpu().numpy()
+pl = env.state()["vm_placement"].cpu().numpy()
+wall_us = st[:, 7] / 1000 / 100.0  # 100 MHz realtime ticks
+cyc = st[:, 9]
+print(f"wave lifetime: {wall_us.mean():.1f} us wall (mean), {cyc.mean():.0f} shader cycles -> "
+      f"{cyc.mean() / wall_us.mean() / 1e3:.2f} GHz")
+print("mean waiting", (pl == 100).sum(1).mean(), "running", (pl < 100).sum(1).mean())

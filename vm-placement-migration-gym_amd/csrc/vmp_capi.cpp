@@ -75,7 +75,7 @@ double loggam_host(double x) {
 
 struct vmp_handle {
   vmp_config cfg;
-  int32_t N, P, V, A, D, W32, vpt;
+  int32_t N, P, V, A, D, W32;
   int32_t device;
   int32_t eval_mode;
   hipStream_t stream;
@@ -87,6 +87,7 @@ struct vmp_handle {
   EnvParams prm;
   uint32_t *scratch_bits;  // for vmp_mask_bool
   PoisConst *pois_dev;
+  uint64_t *stamps;
 };
 
 namespace {
@@ -141,12 +142,14 @@ void carve(vmp_handle *h) {
   EnvParams &p = h->prm;
   const int64_t P = h->P, V = h->V;
   int max_leaves = 1;
-  for (int n = 0; n <= V || n <= P; n++) {
-    int l = pw_leaves(n);
-    if (l > max_leaves) max_leaves = l;
-  }
+  bool deep = (V > 1928 || P > 1928);  // only deeper recursions use the LDS plan
+  if (deep)
+    for (int n = 0; n <= V || n <= P; n++) {
+      int l = pw_leaves(n);
+      if (l > max_leaves) max_leaves = l;
+    }
   p.NW = (int32_t)((P + 63) / 64);
-  p.n_leaf = max_leaves + 8;
+  p.n_leaf = deep ? max_leaves + 8 : 1;
   int64_t off = 0;
   p.off_hdr = (int32_t)off;
   off = align16(off + (int64_t)sizeof(EnvHdr));
@@ -158,31 +161,40 @@ void carve(vmp_handle *h) {
   off = align16(off + 2 * P);            // tc, tm u8
   p.off_ord = (int32_t)off;
   off = align16(off + 2 * P);            // BF visiting order u16
-  p.off_bits = (int32_t)off;
-  off = align16(off + 2 * 101 * 8 * (int64_t)p.NW);  // bc, bm
+  p.off_bits = (int32_t)off;  // fit bitmaps; after the heuristic: NULL list + accepted sizes
+  {
+    const int64_t bits = 2 * 101 * 8 * (int64_t)p.NW, acc = 4 * V;
+    off = align16(off + (bits > acc ? bits : acc));
+  }
   p.off_sort = (int32_t)off;
-  off = align16(off + 4 * 256);          // introsort stacks
+  off = align16(off + 4 * 256);          // introsort stacks (BF)
   p.off_stage = (int32_t)off;
-  off = align16(off + 8 * 64);           // staged accepted VMs
+  off = align16(off + 8 * 16);           // reduction results + draw bookkeeping
   p.off_ccomp = (int32_t)off;
   off = align16(off + 2 * V);            // ccomp, mcomp u8
   p.off_leaf = (int32_t)off;
   off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);  // lo, len, lane-0 stack
   p.off_leafval = (int32_t)off;
   off = align16(off + 8 * 8 * (int64_t)p.n_leaf + 8 * (2 * (int64_t)p.n_leaf + 64));
+  p.off_pre = (int32_t)off;   // per-launch random draws follow (launch_env)
   p.lds_wave_bytes = (int32_t)off;
 }
 
 int launch_env(vmp_handle *h, const StepOut &o) {
   dim3 grid((h->N + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
-  size_t lds = (size_t)h->prm.lds_wave_bytes * kWavesPerBlock;
-  switch (h->vpt) {
-    case 1: hipLaunchKernelGGL(k_env<1>, grid, block, lds, h->stream, h->prm, o); break;
-    case 2: hipLaunchKernelGGL(k_env<2>, grid, block, lds, h->stream, h->prm, o); break;
-    case 4: hipLaunchKernelGGL(k_env<4>, grid, block, lds, h->stream, h->prm, o); break;
-    case 8: hipLaunchKernelGGL(k_env<8>, grid, block, lds, h->stream, h->prm, o); break;
-    default: hipLaunchKernelGGL(k_env<16>, grid, block, lds, h->stream, h->prm, o); break;
-  }
+  EnvParams p = h->prm;
+  // per-launch region: speculative service draws (state + value) and arrivals
+  p.scap = kSpecDraws;
+  const int64_t pre = 20 * (int64_t)p.scap + 4 * (int64_t)(o.k_steps > 0 ? o.k_steps : 1);
+  p.lds_wave_bytes = (int32_t)align16(p.off_pre + pre);
+  size_t lds = (size_t)p.lds_wave_bytes * kWavesPerBlock;
+  if (lds > 160 * 1024 - 2048) return fail(VMP_EINVAL, "config too large for the LDS carve");
+  const int need = (h->V + 63) / 64;
+  if (need <= 1) hipLaunchKernelGGL(k_env<1>, grid, block, lds, h->stream, p, o);
+  else if (need <= 2) hipLaunchKernelGGL(k_env<2>, grid, block, lds, h->stream, p, o);
+  else if (need <= 4) hipLaunchKernelGGL(k_env<4>, grid, block, lds, h->stream, p, o);
+  else if (need <= 8) hipLaunchKernelGGL(k_env<8>, grid, block, lds, h->stream, p, o);
+  else hipLaunchKernelGGL(k_env<16>, grid, block, lds, h->stream, p, o);
   HIP_TRY(hipGetLastError());
   return VMP_OK;
 }
@@ -229,8 +241,6 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   h->A = cfg->allow_null_action ? cfg->pms + 2 : cfg->pms + 1;
   h->D = 3 * cfg->vms + 2 * cfg->pms;
   h->W32 = (h->A + 31) / 32;
-  int need = (h->V + 63) / 64;
-  h->vpt = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : need <= 8 ? 8 : 16;
   h->device = device;
   h->stream = nullptr;
   std::vector<double> t1, t2;
@@ -263,8 +273,6 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   p.seq_lo = cfg->sequence == VMP_SEQ_HIGHUNIFORM ? 0.25 : 0.1;
   double hi = cfg->sequence == VMP_SEQ_LOWUNIFORM ? 0.65 : 1.0;
   p.seq_range = hi - p.seq_lo;  // Generator.uniform: low + (high-low)*u
-  p.arr = h->arr;
-  p.svc = h->svc;
   {
     PoisConst pc[2] = {h->arr, h->svc};
     HIP_TRY(hipMalloc(&h->pois_dev, sizeof(pc)));
@@ -275,6 +283,11 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   p.pm = h->pm;
   p.hdr = h->hdr;
   carve(h);
+#ifdef VMP_STAMPS
+  HIP_TRY(hipMalloc(&h->stamps, sizeof(uint64_t) * 16 * (size_t)n_env));
+  HIP_TRY(hipMemset(h->stamps, 0, sizeof(uint64_t) * 16 * (size_t)n_env));
+  p.stamps = h->stamps;
+#endif
   int maxn = h->V > h->P ? h->V : h->P;
   int depth = 0;
   for (int n = 0; n <= maxn; n++) depth = pw_depth(n) > depth ? pw_depth(n) : depth;
@@ -282,9 +295,10 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
     vmp_destroy(h);
     return fail(VMP_EINVAL, "config exceeds the pairwise-sum recursion depth of this build");
   }
-  if (p.lds_wave_bytes * kWavesPerBlock > 160 * 1024 - 2048) {
+  if ((p.lds_wave_bytes + 20 * kSpecDraws + 4 * kMaxStepsPerLaunch) * kWavesPerBlock >
+      160 * 1024 - 2048) {
     vmp_destroy(h);
-    return fail(VMP_EINVAL, "config too large for the LDS-resident kernel");
+    return fail(VMP_EINVAL, "config too large for the LDS carve of this build");
   }
   refresh_params(h);
   int64_t *dseeds = nullptr;
@@ -308,6 +322,7 @@ int vmp_destroy(vmp_handle *h) {
   (void)hipFree(h->lg_svc);
   (void)hipFree(h->scratch_bits);
   (void)hipFree(h->pois_dev);
+  (void)hipFree(h->stamps);
   delete h;
   return VMP_OK;
 }
@@ -388,12 +403,17 @@ int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double
   if (!h || k_steps < 1) return fail(VMP_EINVAL, "null handle or k_steps < 1");
   if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
     return fail(VMP_EINVAL, "unknown policy");
-  StepOut o = empty_out();
-  o.policy = policy;
-  o.reward = rewards;
-  o.done_count = done_count;
-  o.k_steps = k_steps;
-  return launch_env(h, o);
+  // launches of at most kMaxStepsPerLaunch steps (the per-launch draw region)
+  for (int32_t k0 = 0; k0 < k_steps; k0 += kMaxStepsPerLaunch) {
+    StepOut o = empty_out();
+    o.policy = policy;
+    o.reward = rewards ? rewards + (int64_t)k0 * h->N : nullptr;
+    o.done_count = done_count;
+    o.k_steps = k_steps - k0 < kMaxStepsPerLaunch ? k_steps - k0 : kMaxStepsPerLaunch;
+    int rc = launch_env(h, o);
+    if (rc) return rc;
+  }
+  return VMP_OK;
 }
 
 int vmp_mask(vmp_handle *h, uint32_t *bits) {
@@ -482,6 +502,15 @@ int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
                      dim3(64 * kWavesPerBlock), 0, (hipStream_t)stream, B, V, A, W, logits,
                      mask_bits, seed, offset, action, logprob_row, entropy_row);
   HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_debug_stamps(vmp_handle *h, uint64_t *out) {
+  if (!h || !out) return fail(VMP_EINVAL, "null argument");
+  if (!h->stamps) return fail(VMP_EINVAL, "library built without -DVMP_STAMPS");
+  HIP_TRY(hipMemcpyAsync(out, h->stamps, sizeof(uint64_t) * 16 * (size_t)h->N,
+                         hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(uint64_t) * 16 * (size_t)h->N, h->stream));
   return VMP_OK;
 }
 

@@ -19,7 +19,7 @@
 // Minimum waves per SIMD the env kernel is register-allocated for
 // (__launch_bounds__ 2nd argument); measured choice, see DESIGN.md.
 #ifndef VMP_WAVES_PER_EU
-#define VMP_WAVES_PER_EU 1
+#define VMP_WAVES_PER_EU 2
 #endif
 
 namespace vmp {
@@ -132,7 +132,7 @@ __device__ void pcg_seed(Pcg &r, uint64_t seed) {
 }
 
 // random_loggam (distributions.c) — device fallback outside the host table.
-__device__ __forceinline__ double loggam_dev(double x) {
+__device__ double loggam_dev(double x) {
   const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
                         -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
                         6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
@@ -155,18 +155,32 @@ __device__ __forceinline__ double loggam_dev(double x) {
   return gl;
 }
 
+// loggam beyond the host table (k > lam + 16 sqrt(lam) + 64): never reached in
+// practice; out of line so it costs the env kernel no registers.
+__device__ __noinline__ double loggam_far(double x) { return loggam_dev(x); }
+
+// PTRS acceptance test of random_poisson_ptrs (distributions.c), the branch
+// taken by ~14% of draws: out of line so its log()s do not hold registers in
+// the env kernel. loggam(k+1) comes from the host table (glibc) when in range.
+__device__ __forceinline__ bool ptrs_accept(double V, double us, int64_t k, double lam, double a,
+                                         double b, double loglam, double log_invalpha,
+                                         const double *tab, int tab_n) {
+  const double lg = (k + 1 < tab_n) ? tab[k + 1] : loggam_far((double)(k + 1));
+  return (log(V) + log_invalpha - log(a / (us * us) + b)) <= (-lam + k * loglam - lg);
+}
+
 // random_poisson (distributions.c): mult method (lam < 10) / PTRS (lam >= 10).
 __device__ __forceinline__ int64_t poisson(Pcg &r, const PoisConst &c) {
   if (c.kind == 2) {
+#pragma unroll 1
     for (;;) {
-      double U = next_double(r) - 0.5;
-      double V = next_double(r);
-      double us = 0.5 - fabs(U);
-      int64_t k = (int64_t)floor((2 * c.a / us + c.b) * U + c.lam + 0.43);
+      const double U = next_double(r) - 0.5;
+      const double V = next_double(r);
+      const double us = 0.5 - fabs(U);
+      const int64_t k = (int64_t)floor((2 * c.a / us + c.b) * U + c.lam + 0.43);
       if ((us >= 0.07) && (V <= c.vr)) return k;
       if ((k < 0) || ((us < 0.013) && (V > us))) continue;
-      double lg = (k + 1 < c.tab_n) ? c.loggam_tab[k + 1] : loggam_dev((double)(k + 1));
-      if ((log(V) + c.log_invalpha - log(c.a / (us * us) + c.b)) <= (-c.lam + k * c.loglam - lg))
+      if (ptrs_accept(V, us, k, c.lam, c.a, c.b, c.loglam, c.log_invalpha, c.loggam_tab, c.tab_n))
         return k;
     }
   } else if (c.kind == 0) {
@@ -174,6 +188,7 @@ __device__ __forceinline__ int64_t poisson(Pcg &r, const PoisConst &c) {
   }
   double prod = 1.0;
   int64_t X = 0;
+#pragma unroll 1
   for (;;) {
     prod *= next_double(r);
     if (prod > c.enlam)
@@ -200,6 +215,27 @@ __device__ __forceinline__ int64_t poisson_lds(uint64_t *hdr_rng, const PoisCons
   __builtin_amdgcn_wave_barrier();
   return x;
 }
+
+// Diagnostic build only (-DVMP_STAMPS): per-phase shader-clock deltas,
+// accumulated per env into p.stamps[e][8]. No stamp executes otherwise.
+#ifdef VMP_STAMPS
+#define STAMP_DECL uint64_t st_acc[16] = {0}, st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                   \
+  do {                                             \
+    const uint64_t _t = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += _t - st_prev;                     \
+    st_prev = _t;                                  \
+  } while (0)
+#define STAMP_FLUSH()                                                         \
+  do {                                                                        \
+    if (p.stamps && lane == 0)                                                \
+      for (int _i = 0; _i < 16; _i++) p.stamps[(int64_t)e * 16 + _i] += st_acc[_i]; \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH()
+#endif
 
 // ---------------------------------------------------- pairwise summation --
 // numpy DOUBLE_pairwise_sum (loops_utils.h.src, PW_BLOCKSIZE 128) of
@@ -271,53 +307,138 @@ __device__ __forceinline__ double pw_combine(int n, const PwLds &S, int nl) {
   return vs[0];
 }
 
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const int64_t b = __double_as_longlong(x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
+}
+
+// Register-resident plan (depth <= kPwRegDepth, i.e. n <= 1928): leaf cnt's
+// (offset, size) lands in lane cnt; the combine reads leaf sums by readlane.
+constexpr int kPwRegDepth = 4;
+template <int D>
+__device__ __forceinline__ void pw_enum_r(int o, int n, int &cnt, int lane, int &my_o,
+                                          int &my_m) {
+  if (D == 0 || n <= 128) {
+    if (lane == cnt) {
+      my_o = o;
+      my_m = n;
+    }
+    cnt++;
+    return;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  pw_enum_r<(D > 0 ? D - 1 : 0)>(o, n2, cnt, lane, my_o, my_m);
+  pw_enum_r<(D > 0 ? D - 1 : 0)>(o + n2, n - n2, cnt, lane, my_o, my_m);
+}
+template <int D>
+__device__ __forceinline__ double pw_comb_r(int n, int &cnt, double myval) {
+  if (D == 0 || n <= 128) return readlane_f64(myval, cnt++);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  const double a = pw_comb_r<(D > 0 ? D - 1 : 0)>(n2, cnt, myval);
+  const double b = pw_comb_r<(D > 0 ? D - 1 : 0)>(n - n2, cnt, myval);
+  return a + b;
+}
+
+// One leaf [o, o+m) by the 8-lane group of the calling lane; the value is
+// valid in the group's lane j == 0. Chain loads are issued 8 at a time.
+template <class F>
+__device__ __forceinline__ double pw_leaf_group(int o, int m, F &f) {
+  const int j = lane_id() & 7;
+  const int full = m - (m % 8);
+  const int cnt = full >> 3;  // elements per accumulator chain (<= 16)
+  double r = 0.0;
+  if (cnt > 0) {
+    double x[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) x[t] = t < cnt ? f(o + j + 8 * t) : 0.0;
+    r = x[0];
+#pragma unroll
+    for (int t = 1; t < 8; t++)
+      if (t < cnt) r += x[t];
+    if (cnt > 8) {
+#pragma unroll
+      for (int t = 0; t < 8; t++) x[t] = t + 8 < cnt ? f(o + j + 8 * (t + 8)) : 0.0;
+#pragma unroll
+      for (int t = 0; t < 8; t++)
+        if (t + 8 < cnt) r += x[t];
+    }
+  }
+  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)): xor-pairs reproduce the tree exactly
+  // (f64 addition is commutative)
+  r = r + __shfl_xor(r, 1);
+  r = r + __shfl_xor(r, 2);
+  r = r + __shfl_xor(r, 4);
+  double res = cnt > 0 ? r : 0.0;
+  if (j == 0) {
+    double tl[7];
+#pragma unroll
+    for (int t = 0; t < 7; t++) tl[t] = full + t < m ? f(o + full + t) : 0.0;
+#pragma unroll
+    for (int t = 0; t < 7; t++)
+      if (full + t < m) res += tl[t];
+  }
+  return res;
+}
+
 template <class F>
 __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
   const int lane = lane_id();
+  if (n <= 128) return readlane_f64(pw_leaf_group(0, n, f), 0);
+  if (n <= 1928) {
+    int my_o = 0, my_m = 0, nl = 0;
+    pw_enum_r<kPwRegDepth>(0, n, nl, lane, my_o, my_m);
+    double myval = 0.0;
+    for (int b = 0; b < nl; b += 8) {
+      const int l = b + (lane >> 3);
+      const int o = __shfl(my_o, l & 63), m = l < nl ? __shfl(my_m, l & 63) : 0;
+      const double v = pw_leaf_group(o, m, f);
+      const double moved = __shfl(v, ((lane - b) & 7) * 8);
+      if (lane >= b && lane < b + 8) myval = moved;
+    }
+    int cnt = 0;
+    return pw_comb_r<kPwRegDepth>(n, cnt, myval);
+  }
+  // deeper recursion (n > 1928, P-sized sums of big configs): LDS plan
   int nl = 1;
-  if (n > 128) {
-    if (lane == 0) S.stk[191] = pw_plan(n, S);
-    wsync();
-    nl = S.stk[191];
-  }
-  const int j = lane & 7;
-  for (int b = 0; b < nl; b += 8) {  // accumulator chains, 8 leaves per pass
+  if (lane == 0) S.stk[191] = pw_plan(n, S);
+  wsync();
+  nl = S.stk[191];
+  for (int b = 0; b < nl; b += 8) {
     const int l = b + (lane >> 3);
-    if (l < nl) {
-      const int o = nl == 1 ? 0 : S.lo[l], m = nl == 1 ? n : S.len[l];
-      const int full = m - (m % 8);
-      double r = 0.0;
-      if (m >= 8) {
-        r = f(o + j);
-        for (int i = o + j + 8; i < o + full; i += 8) r += f(i);
-      }
-      S.acc[l * 8 + j] = r;
-    }
+    const int o = l < nl ? S.lo[l] : 0, m = l < nl ? S.len[l] : 0;
+    const double v = pw_leaf_group(o, m, f);
+    if (l < nl && (lane & 7) == 0) S.val[l] = v;
   }
   wsync();
-  for (int l = lane; l < nl; l += 64) {  // leaf combine + sequential tail
-    const int o = nl == 1 ? 0 : S.lo[l], m = nl == 1 ? n : S.len[l];
-    const double *a = S.acc + l * 8;
-    double res;
-    int i0;
-    if (m < 8) {
-      res = 0.0;
-      i0 = o;
-    } else {
-      res = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
-      i0 = o + m - (m % 8);
-    }
-    for (int i = i0; i < o + m; i++) res += f(i);
-    S.val[l] = res;
-  }
+  if (lane == 0) S.val[nl] = pw_combine(n, S, nl);
   wsync();
-  if (nl > 1) {
-    if (lane == 0) S.val[nl] = pw_combine(n, S, nl);
-    wsync();
-  }
-  const double r = S.val[nl > 1 ? nl : 0];
+  const double r = S.val[nl];
   wsync();
   return r;
+}
+
+// The reductions of one step, through ONE out-of-line body: x(i) is
+// cent[u8[i]] (VM sizes) or f64[i] (PM resources), optionally (x - mean)^2.
+enum PwKind { PW_U8 = 0, PW_F64 = 1, PW_U8_SQDEV = 2, PW_F64_SQDEV = 3 };
+__device__ __forceinline__ double pw_sum(int n, int kind, const void *src, const double *cent,
+                                         double mean, PwLds S) {
+  const uint8_t *u8 = (const uint8_t *)src;
+  const double *f64 = (const double *)src;
+  return wave_pw_sum(
+      n,
+      [=](int i) {
+        double x = (kind & 1) ? f64[i] : cent[u8[i]];
+        if (kind & 2) {
+          const double d = x - mean;
+          x = d * d;
+        }
+        return x;
+      },
+      S);
 }
 
 // ------------------------------------------- numpy scalar argsort (BF) ----
@@ -425,10 +546,54 @@ struct Lds {
   uint16_t *ord;           // BF ascending argsort, then reversed into visiting order
   uint64_t *bc, *bm;       // [101][NW] fit bitmaps by size (bit = visiting position)
   int32_t *sortstk;        // introsort stacks
-  uint64_t *stage;         // 64 staged accepted-VM words
+  uint16_t *nulls;         // NULL slot indices (aliases the fit bitmaps)
+  uint8_t *accc, *accm;    // accepted sizes (alias the fit bitmaps)
+  double *jobres;          // reduction results of the step
+  int32_t *arr;            // per-step arrivals of the launch (prologue draws)
+  uint32_t *svc;           // speculative planned runtimes
+  uint64_t *svcst;         // rng4 state after each speculative draw
+  uint64_t *svcfb;         // rng4 state for fallback draws
+  int32_t *svcinfo;        // [0] speculative count, [1] consumed
   uint8_t *ccomp, *mcomp;  // compressed sizes of existing VMs [V]
   PwLds pw;
+  char *base;              // the wave's LDS region
 };
+
+// The wave's LDS view, rebuilt from its base address (cheap; avoids passing
+// the pointer struct by value into out-of-line helpers).
+__device__ __forceinline__ Lds make_lds(const EnvParams &p, char *base) {
+  Lds L;
+  L.hdr = reinterpret_cast<EnvHdr *>(base + p.off_hdr);
+  L.cpu = reinterpret_cast<double *>(base + p.off_pm);
+  L.mem = L.cpu + p.P;
+  L.fcpu = reinterpret_cast<float *>(base + p.off_fpm);
+  L.fmem = L.fcpu + p.P;
+  L.fkey = L.fmem + p.P;
+  L.tc = reinterpret_cast<uint8_t *>(base + p.off_thr);
+  L.tm = L.tc + p.P;
+  L.ord = reinterpret_cast<uint16_t *>(base + p.off_ord);
+  L.bc = reinterpret_cast<uint64_t *>(base + p.off_bits);
+  L.bm = L.bc + 101 * p.NW;
+  L.sortstk = reinterpret_cast<int32_t *>(base + p.off_sort);
+  L.nulls = reinterpret_cast<uint16_t *>(base + p.off_bits);
+  L.accc = reinterpret_cast<uint8_t *>(base + p.off_bits) + 2 * p.V;
+  L.accm = L.accc + p.V;
+  L.jobres = reinterpret_cast<double *>(base + p.off_stage);
+  L.svcinfo = reinterpret_cast<int32_t *>(base + p.off_stage + 8 * 12);
+  L.svcfb = reinterpret_cast<uint64_t *>(base + p.off_stage + 8 * 14);
+  L.svcst = reinterpret_cast<uint64_t *>(base + p.off_pre);
+  L.svc = reinterpret_cast<uint32_t *>(base + p.off_pre + 16 * p.scap);
+  L.arr = reinterpret_cast<int32_t *>(base + p.off_pre + 20 * p.scap);
+  L.ccomp = reinterpret_cast<uint8_t *>(base + p.off_ccomp);
+  L.mcomp = L.ccomp + p.V;
+  L.pw.lo = reinterpret_cast<int32_t *>(base + p.off_leaf);
+  L.pw.len = L.pw.lo + p.n_leaf;
+  L.pw.stk = L.pw.len + p.n_leaf;
+  L.pw.acc = reinterpret_cast<double *>(base + p.off_leafval);
+  L.pw.val = L.pw.acc + 8 * p.n_leaf;
+  L.base = base;
+  return L;
+}
 
 // Exact k/100 for k = 0..127 (np.around(., 2) values), per block.
 struct Tables {
@@ -456,37 +621,73 @@ __device__ __forceinline__ void st_pcg(EnvHdr *h, int k, const Pcg &r) {
   }
 }
 
-// Largest k in [0, 100] with f + FC[k] <= 1 in f32 (monotone in k), or -1.
+// Largest k in [0, 100] with f + FC[k] <= 1 in f32 (monotone in k), or -1:
+// start from the estimate (1-f)*100 and walk (almost always 0-1 steps).
 __device__ __forceinline__ int fit_threshold(float f, const float *fc) {
-  if (!(f + fc[0] <= 1.0f)) return -1;
-  int lo = 0, hi = 101;
-  while (hi - lo > 1) {
-    int mid = (lo + hi) >> 1;
-    if (f + fc[mid] <= 1.0f) lo = mid; else hi = mid;
+  int k = (int)((1.0f - f) * 100.0f);
+  k = k < 0 ? 0 : (k > 100 ? 100 : k);
+  if (f + fc[k] <= 1.0f) {
+#pragma unroll 1
+    while (k < 100 && f + fc[k + 1] <= 1.0f) k++;
+    return k;
   }
-  return lo;
+#pragma unroll 1
+  while (k > 0 && !(f + fc[k - 1] <= 1.0f)) k--;
+  return k - 1;
+}
+
+__device__ __forceinline__ uint64_t shfl_down_u64(uint64_t x, int d) {
+  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)x, d);
+  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(x >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+// Suffix OR across the wave: lane k gets OR of x over lanes >= k.
+__device__ __forceinline__ uint64_t suffix_or(uint64_t x) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = shfl_down_u64(x, d);
+    if (lane + d < 64) x |= y;
+  }
+  return x;
 }
 
 // Rebuild the fit bitmaps: bit i of bc[k][w] is set iff the PM at visiting
-// position w*64+i accepts a VM of cpu size k/100 (f32 obs arithmetic).
-__device__ __forceinline__ void build_bitmaps(const EnvParams &p, const Lds &L, bool bf) {
+// position w*64+i accepts a VM of cpu size k/100 (f32 obs arithmetic), i.e.
+// iff its threshold tc >= k. PMs are bucketed by threshold with LDS atomic
+// ORs, then a suffix OR over k (lanes) turns buckets into "tc >= k" masks.
+__device__ __forceinline__ void build_bitmaps(const EnvParams &p, char *lbase, bool bf) {
+  const Lds L = make_lds(p, lbase);
   const int lane = lane_id();
   const int P = p.P, NW = p.NW;
+  for (int i = lane; i < 101 * NW; i += 64) {
+    L.bc[i] = 0;
+    L.bm[i] = 0;
+  }
+  wsync();
   for (int w = 0; w < NW; w++) {
-    int pos = w * 64 + lane;
-    int q = pos < P ? (bf ? (int)L.ord[pos] : pos) : 0;
-    int tcq = pos < P ? (int)L.tc[q] - 1 : -1;
-    int tmq = pos < P ? (int)L.tm[q] - 1 : -1;
-    uint64_t c0 = 0, c1 = 0, m0 = 0, m1 = 0;
-    for (int k = 0; k < 101; k++) {
-      uint64_t bcw = ballot(tcq >= k), bmw = ballot(tmq >= k);
-      if ((k & 63) == lane) {
-        if (k < 64) { c0 = bcw; m0 = bmw; } else { c1 = bcw; m1 = bmw; }
-      }
+    const int pos = w * 64 + lane;
+    if (pos < P) {
+      const int q = bf ? (int)L.ord[pos] : pos;
+      const int tcq = (int)L.tc[q] - 1, tmq = (int)L.tm[q] - 1;
+      if (tcq >= 0) atomicOr((unsigned long long *)&L.bc[tcq * NW + w], 1ull << lane);
+      if (tmq >= 0) atomicOr((unsigned long long *)&L.bm[tmq * NW + w], 1ull << lane);
     }
+  }
+  wsync();
+  for (int w = 0; w < NW; w++) {
+    const bool hi_ok = lane + 64 < 101;
+    uint64_t c1 = hi_ok ? L.bc[(lane + 64) * NW + w] : 0, m1 = hi_ok ? L.bm[(lane + 64) * NW + w] : 0;
+    uint64_t c0 = L.bc[lane * NW + w], m0 = L.bm[lane * NW + w];
+    c1 = suffix_or(c1);
+    m1 = suffix_or(m1);
+    const uint64_t ct = (uint64_t)__shfl((long long)c1, 0), mt = (uint64_t)__shfl((long long)m1, 0);
+    c0 = suffix_or(c0) | ct;
+    m0 = suffix_or(m0) | mt;
+    wsync();
     L.bc[lane * NW + w] = c0;
     L.bm[lane * NW + w] = m0;
-    if (lane + 64 < 101) {
+    if (hi_ok) {
       L.bc[(lane + 64) * NW + w] = c1;
       L.bm[(lane + 64) * NW + w] = m1;
     }
@@ -496,6 +697,12 @@ __device__ __forceinline__ void build_bitmaps(const EnvParams &p, const Lds &L, 
 
 // First visiting position accepting sizes (kc, km), or -1.
 __device__ __forceinline__ int bm_query(const Lds &L, int NW, int kc, int km) {
+  if (NW <= 2) {  // P <= 128: both words at once, no early exit
+    const uint64_t a0 = L.bc[kc * NW] & L.bm[km * NW];
+    const uint64_t a1 = NW == 2 ? (L.bc[kc * NW + 1] & L.bm[km * NW + 1]) : 0ull;
+    return a0 ? __ffsll((unsigned long long)a0) - 1
+              : (a1 ? 64 + __ffsll((unsigned long long)a1) - 1 : -1);
+  }
   for (int w = 0; w < NW; w++) {
     uint64_t m = L.bc[kc * NW + w] & L.bm[km * NW + w];
     if (m) return w * 64 + __ffsll((unsigned long long)m) - 1;
@@ -503,7 +710,8 @@ __device__ __forceinline__ int bm_query(const Lds &L, int NW, int kc, int km) {
   return -1;
 }
 
-__device__ __forceinline__ void bf_sort(const EnvParams &p, const Lds &L) {
+__device__ __forceinline__ void bf_sort(const EnvParams &p, char *lbase) {
+  const Lds L = make_lds(p, lbase);
   const int lane = lane_id();
   const int P = p.P;
   for (int i = lane; i < P; i += 64) L.fkey[i] = L.fcpu[i] + L.fmem[i];
@@ -536,6 +744,103 @@ __device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int q, 
   return ok;
 }
 
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// ---- random draws of a launch (prologue) ---------------------------------
+// All Poisson draws a launch can need are taken BEFORE the VM state is loaded
+// into registers, so the samplers never share the register budget with it:
+// the K arrival counts (rng3, one per step, all consumed) and up to scap
+// service lengths (rng4), speculative: only the first `used` are consumed and
+// rng4 is committed to the state recorded after draw used-1 (draws past scap
+// come from the out-of-line fallback below).
+__device__ __noinline__ uint32_t svc_fallback(uint64_t *st, const uint64_t *inc,
+                                              const PoisConst *c) {
+  Pcg r;
+  r.s = U128{st[0], st[1]};
+  r.inc = U128{inc[0], inc[1]};
+  const int64_t x = poisson(r, *c);
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if ((threadIdx.x & 63) == 0) {
+    st[0] = r.s.hi;
+    st[1] = r.s.lo;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  return (uint32_t)(x + 1);
+}
+
+__device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, int K, int V) {
+  const int lane = lane_id();
+  EnvHdr *H = L.hdr;
+  Pcg r3 = ld_pcg(H, 2);
+  int64_t need = 0;
+#pragma unroll 1
+  for (int k = 0; k < K; k++) {
+    const int64_t a = poisson(r3, p.pois[0]);
+    if (lane == 0) L.arr[k] = (int32_t)(a < 0x7fffffff ? a : 0x7fffffff);
+    need += a < V ? a : V;
+  }
+  st_pcg(H, 2, r3);
+  Pcg r4 = ld_pcg(H, 3);
+  const int S = (int)(need < p.scap ? need : p.scap);
+#pragma unroll 1
+  for (int j = 0; j < S; j++) {
+    const int64_t x = poisson(r4, p.pois[1]);
+    if (lane == 0) {
+      L.svc[j] = (uint32_t)(x + 1);
+      L.svcst[2 * j] = r4.s.hi;
+      L.svcst[2 * j + 1] = r4.s.lo;
+    }
+  }
+  if (lane == 0) {
+    L.svcfb[0] = r4.s.hi;  // fallback continues after the last speculative draw
+    L.svcfb[1] = r4.s.lo;
+    L.svcinfo[0] = S;
+    L.svcinfo[1] = 0;  // consumed
+  }
+  wsync();
+}
+
+// Next planned runtime (rng4.poisson(L) + 1, env.py:289) for an accepted VM.
+__device__ __forceinline__ uint32_t svc_take(const EnvParams &p, const Lds &L) {
+  const int S = L.svcinfo[0], used = L.svcinfo[1];
+  uint32_t x;
+  if (used < S) {
+    x = L.svc[used];
+  } else {
+    x = svc_fallback(L.svcfb, &L.hdr->rng[3][2], p.pois + 1);
+  }
+  wsync();
+  if (lane_id() == 0) L.svcinfo[1] = used + 1;
+  wsync();
+  return x;
+}
+
+// Commit rng4 to the state after the last consumed draw.
+__device__ __forceinline__ void svc_commit(const Lds &L) {
+  const int S = L.svcinfo[0], used = L.svcinfo[1];
+  if (used == 0) return;
+  uint64_t hi, lo;
+  if (used <= S) {
+    hi = L.svcst[2 * (used - 1)];
+    lo = L.svcst[2 * (used - 1) + 1];
+  } else {
+    hi = L.svcfb[0];
+    lo = L.svcfb[1];
+  }
+  wsync();
+  if (lane_id() == 0) {
+    L.hdr->rng[3][0] = hi;
+    L.hdr->rng[3][1] = lo;
+  }
+  wsync();
+}
+
 // FirstFitAgent.act / BestFitAgent.act (firstfit.py:21-38, bestfit.py:21-40)
 // on the pre-step f32 observation, fused with the action phase of step().
 // Exact w.r.t. the reference's sequential loop because:
@@ -546,9 +851,10 @@ __device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int q, 
 //    so applying each winner's env event as soon as it is decided equals
 //    deciding every action first and stepping afterwards (env.py:68-88).
 template <int VPT>
-__device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds &L, const Tables &T,
-                                   uint32_t (&wa)[VPT], int policy, int32_t *act_out,
-                                   uint8_t *valid_out) {
+__device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds &L,
+                                                   const Tables &T, uint32_t (&wa)[VPT],
+                                                   int policy, int32_t *act_out,
+                                                   uint8_t *valid_out) {
   const int lane = lane_id();
   const int P = p.P, V = p.V, WAIT = p.P, NW = p.NW;
   const bool bf = policy == 1;
@@ -560,26 +866,35 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
   int64_t n_place = 0;
   if (ballot(pend != 0)) {
     for (int i = lane; i < P; i += 64) {
-      float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
+      const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
       L.fcpu[i] = fcv;
       L.fmem[i] = fmv;
       L.tc[i] = (uint8_t)(fit_threshold(fcv, T.fcent) + 1);
       L.tm[i] = (uint8_t)(fit_threshold(fmv, T.fcent) + 1);
     }
     wsync();
-    if (bf) bf_sort(p, L);
-    build_bitmaps(p, L, bf);
+    bool rebuild = true;
+#pragma unroll 1
     for (;;) {
+      if (rebuild) {  // single site: initial build, and BF's re-sort after a win
+        if (bf) bf_sort(p, L.base);
+        build_bitmaps(p, L.base, bf);
+        rebuild = false;
+      }
       int ws = -1, wl = 0, wpos = 0;
+      uint32_t ww = 0;
 #pragma unroll
       for (int s = 0; s < VPT; s++) {
-        bool pd = (pend >> s) & 1u;
-        int pos = pd ? bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) : -1;
-        uint64_t m = ballot(pos >= 0);
-        if (ws < 0 && m) {
-          ws = s;
-          wl = __ffsll((unsigned long long)m) - 1;
-          wpos = __builtin_amdgcn_readlane(pos, wl);
+        const bool pd = (pend >> s) & 1u;
+        if (ws < 0 && ballot(pd)) {
+          const int pos = pd ? bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) : -1;
+          const uint64_t m = ballot(pos >= 0);
+          if (m) {
+            ws = s;
+            wl = __ffsll((unsigned long long)m) - 1;
+            wpos = __builtin_amdgcn_readlane(pos, wl);
+            ww = rdlane(wa[s], wl);
+          }
         }
       }
       if (ws < 0) break;
@@ -587,14 +902,9 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
 #pragma unroll
       for (int s = 0; s < VPT; s++)
         if (s < ws || (s == ws && lane <= wl)) pend &= ~(1u << s);
-      uint32_t ww = 0;
-#pragma unroll
-      for (int s = 0; s < VPT; s++)
-        if (s == ws) ww = rdlane(wa[s], wl);
       const int kc = w_cc(ww), km = w_cm(ww);
       const int q = bf ? (int)L.ord[wpos] : wpos;
-      // env event, f64 (env.py:55-56, 58-64)
-      bool ok = env_place(L, T, q, kc, km);
+      const bool ok = env_place(L, T, q, kc, km);  // env.py:55-56, 58-64
       n_place += ok;
       if (lane == wl) {
 #pragma unroll
@@ -608,37 +918,38 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
       }
       // heuristic state update (f32): FF updates cpu only (firstfit.py:36)
       if (lane == 0) {
-        float nc = L.fcpu[q] + T.fcent[kc];
+        const float nc = L.fcpu[q] + T.fcent[kc];
         L.fcpu[q] = nc;
         L.tc[q] = (uint8_t)(fit_threshold(nc, T.fcent) + 1);
         if (bf) {
-          float nm = L.fmem[q] + T.fcent[km];
+          const float nm = L.fmem[q] + T.fcent[km];
           L.fmem[q] = nm;
           L.tm[q] = (uint8_t)(fit_threshold(nm, T.fcent) + 1);
         }
       }
       wsync();
       if (bf) {
-        bf_sort(p, L);
-        build_bitmaps(p, L, true);
+        rebuild = true;
       } else {  // only PM q's bit changes, for sizes above its new threshold
         const int t = (int)L.tc[q] - 1;
         const int w = q >> 6;
         const uint64_t bit = 1ull << (q & 63);
         for (int k = lane; k < 101; k += 64) {
-          uint64_t x = L.bc[k * NW + w];
+          const uint64_t x = L.bc[k * NW + w];
           L.bc[k * NW + w] = (t >= k) ? (x | bit) : (x & ~bit);
         }
         wsync();
       }
     }
   }
+  if (act_out || valid_out) {
 #pragma unroll
-  for (int s = 0; s < VPT; s++) {
-    int v = s * 64 + lane;
-    if (v < V) {
-      if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(wa[s]);
-      if (valid_out) valid_out[v] = (uint8_t)!((bad >> s) & 1u);
+    for (int s = 0; s < VPT; s++) {
+      const int v = s * 64 + lane;
+      if (v < V) {
+        if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(wa[s]);
+        if (valid_out) valid_out[v] = (uint8_t)!((bad >> s) & 1u);
+      }
     }
   }
   return n_place;
@@ -649,8 +960,9 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
 // in ascending VM order by a wave-uniform loop over the ballot.
 template <int VPT>
 __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L, const Tables &T,
-                               uint32_t (&wa)[VPT], const int32_t *act_row, uint8_t *valid_out,
-                               int64_t &n_place, int64_t &n_susp) {
+                                               uint32_t (&wa)[VPT], const int32_t *act_row,
+                                               uint8_t *valid_out, int64_t &n_place,
+                                               int64_t &n_susp) {
   const int lane = lane_id();
   const int P = p.P, V = p.V, WAIT = p.P;
 #pragma unroll
@@ -664,6 +976,7 @@ __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L,
     uint64_t evm = ballot(isplace || issusp);
     uint64_t okm = 0;
     const uint32_t me = wa[s];
+#pragma unroll 1
     while (evm) {  // wave-uniform, ascending lane = ascending VM index
       const int l = __ffsll((unsigned long long)evm) - 1;
       evm &= evm - 1;
@@ -701,7 +1014,6 @@ __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L,
   }
 }
 
-
 // kl_divergence (env.py:8-17) in numpy/LAPACK/OpenBLAS evaluation order.
 __device__ __forceinline__ double kl_reward(double tcm, double tmm, double tcv, double tmv,
                                             double cm, double mm, double cv, double mv) {
@@ -715,35 +1027,16 @@ __device__ __forceinline__ double kl_reward(double tcm, double tmm, double tcv, 
   return -kl;
 }
 
-// kl reward branch (env.py:124-149), out of line: it runs only for
-// reward_function == "kl" and is register-heavy (six reductions, log/exp).
-__device__ __forceinline__ double kl_block(const double *cpu, const double *mem, int P,
-                                        const uint8_t *ccp, const uint8_t *cmp,
-                                        const double *cent, int n_ex, double sum_c,
-                                        double sum_m, double tcm, double tmm, PwLds S) {
-  const double cm_ = wave_pw_sum(P, [=](int i) { return cpu[i]; }, S) / (double)P;
-  const double mm_ = wave_pw_sum(P, [=](int i) { return mem[i]; }, S) / (double)P;
-  double cv = wave_pw_sum(P, [=](int i) { double d = cpu[i] - cm_; return d * d; }, S) /
-              (double)P;
-  double mv = wave_pw_sum(P, [=](int i) { double d = mem[i] - mm_; return d * d; }, S) /
-              (double)P;
-  if (cv == 0) cv = 1e-6;
-  if (mv == 0) mv = 1e-6;
-  const double mc = sum_c / (double)n_ex, mmv = sum_m / (double)n_ex;
-  double tcv = wave_pw_sum(n_ex, [=](int i) { double d = cent[ccp[i]] - mc; return d * d; }, S) /
-               (double)n_ex;
-  double tmv = wave_pw_sum(n_ex, [=](int i) { double d = cent[cmp[i]] - mmv; return d * d; }, S) /
-               (double)n_ex;
-  if (tcv == 0) tcv = 1e-6;
-  if (tmv == 0) tmv = 1e-6;
-  return (tcm == 0 || tmm == 0) ? 0.0 : kl_reward(tcm, tmm, tcv, tmv, cm_, mm_, cv, mv);
-}
-
 // Everything of step() after the action phase: _run_vms, _accept_vm_requests,
 // stats + reward, termination (env.py:101, 108-163, 244-293).
 template <int VPT>
 __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, const Tables &T,
-                           uint32_t (&wa)[VPT], uint32_t (&rem)[VPT], bool &terminated) {
+                                           uint32_t (&wa)[VPT], uint32_t (&rem)[VPT],
+                                           int kstep, bool &terminated
+#ifdef VMP_STAMPS
+                                           , uint64_t (&st_acc)[16], uint64_t &st_prev
+#endif
+) {
   const int lane = lane_id();
   const int P = p.P, V = p.V, WAIT = p.P, NUL = p.P + 1;
   EnvHdr *H = L.hdr;
@@ -758,6 +1051,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     uint64_t it = ballot(term);
     n_term += __popcll(it);
     const uint32_t me = wa[s];
+#pragma unroll 1
     while (it) {  // frees in ascending VM order (env.py:260-262)
       const int l = __ffsll((unsigned long long)it) - 1;
       it &= it - 1;
@@ -781,70 +1075,57 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     if (L.cpu[i] < 1e-7) L.cpu[i] = 0;
     if (L.mem[i] < 1e-7) L.mem[i] = 0;
   }
+  STAMP(2);
   // ---- _accept_vm_requests (env.py:271-293) ----
-  const int64_t arrivals = poisson_lds(H->rng[2], p.pois + 0);
   int n_null = 0;
 #pragma unroll
-  for (int s = 0; s < VPT; s++)
-    n_null += __popcll(ballot(s * 64 + lane < V && w_pl(wa[s]) == NUL));
+  for (int s = 0; s < VPT; s++) {
+    const int v = s * 64 + lane;
+    const bool isnull = v < V && w_pl(wa[s]) == NUL;
+    const uint64_t nm = ballot(isnull);
+    if (isnull) L.nulls[n_null + below(nm, lane)] = (uint16_t)v;
+    n_null += __popcll(nm);
+  }
+  const int64_t arrivals = L.arr[kstep];  // rng3.poisson(lambda), drawn in the prologue
   const int64_t k = arrivals < n_null ? arrivals : n_null;
   wsync();
   if (k > 0) {
-    // ranks of the NULL slots in ascending VM order (to_accept, env.py:276-277)
-    int rk[VPT];
-    int base = 0;
+    // to_accept = the first k NULL slots; sizes popped from the rng1/rng2
+    // sequences, planned runtimes from rng4 (env.py:276-290)
+    Pcg r1 = ld_pcg(H, 0), r2 = ld_pcg(H, 1);
+#pragma unroll 1
+    for (int j = 0; j < k; j++) {
+      const int cc = (int)rint((p.seq_lo + p.seq_range * next_double(r1)) * 100.0);
+      const int cm = (int)rint((p.seq_lo + p.seq_range * next_double(r2)) * 100.0);
+      const uint32_t rr = svc_take(p, L);
+      const int v = L.nulls[j];
+      if (lane == (v & 63)) {
 #pragma unroll
-    for (int s = 0; s < VPT; s++) {
-      const bool isnull = s * 64 + lane < V && w_pl(wa[s]) == NUL;
-      const uint64_t nm = ballot(isnull);
-      rk[s] = isnull ? base + below(nm, lane) : -1;
-      base += __popcll(nm);
-    }
-    // draws in to_accept order, 64 per chunk: sizes from rng1/rng2 (the popped
-    // sequences, env.py:279-287) and planned runtimes from rng4 (env.py:289)
-    for (int c0 = 0; c0 < k; c0 += 64) {
-      const int cn = (int)(k - c0 < 64 ? k - c0 : 64);
-      Pcg r1 = ld_pcg(H, 0), r2 = ld_pcg(H, 1);
-      for (int j = 0; j < cn; j++) {
-        const int cc = (int)rint((p.seq_lo + p.seq_range * next_double(r1)) * 100.0);
-        const int cm = (int)rint((p.seq_lo + p.seq_range * next_double(r2)) * 100.0);
-        const uint32_t rr = (uint32_t)(poisson_lds(H->rng[3], p.pois + 1) + 1);
-        if (lane == 0) {
-          L.stage[j] = (uint64_t)w_make(WAIT, cc, cm) | ((uint64_t)rr << 32);
-          L.ccomp[c0 + j] = (uint8_t)cc;
-          L.mcomp[c0 + j] = (uint8_t)cm;
-        }
+        for (int s = 0; s < VPT; s++)
+          if (s == (v >> 6)) {
+            wa[s] = w_make(WAIT, cc, cm);
+            rem[s] = rr;
+          }
       }
-      st_pcg(H, 0, r1);
-      st_pcg(H, 1, r2);
-      wsync();
-#pragma unroll
-      for (int s = 0; s < VPT; s++) {
-        if (rk[s] >= c0 && rk[s] < c0 + cn) {
-          const uint64_t w = L.stage[rk[s] - c0];
-          wa[s] = (uint32_t)w;
-          rem[s] = (uint32_t)(w >> 32);
-        }
+      if (lane == 0) {
+        L.accc[j] = (uint8_t)cc;
+        L.accm[j] = (uint8_t)cm;
       }
-      wsync();
     }
-    const uint8_t *ccp = L.ccomp, *cmp = L.mcomp;
-    const double *cent = T.cent;
-    const double sc = wave_pw_sum((int)k, [=](int i) { return cent[ccp[i]]; }, L.pw);
-    const double sm = wave_pw_sum((int)k, [=](int i) { return cent[cmp[i]]; }, L.pw);
-    if (lane == 0) {
-      H->total_cpu_req = H->total_cpu_req + sc;
-      H->total_mem_req = H->total_mem_req + sm;
-    }
+    st_pcg(H, 0, r1);
+    st_pcg(H, 1, r2);
   }
+  wsync();
+  STAMP(3);
   // ---- stats + reward (env.py:112-156) ----
   int n_ex = 0, n_w = 0;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const bool in = s * 64 + lane < V;
     const int c = w_pl(wa[s]);
-    const uint64_t em = ballot(in && c <= WAIT);
-    if (in && c <= WAIT) {
+    const bool ex = in && c <= WAIT;
+    const uint64_t em = ballot(ex);
+    if (ex) {
       const int rk = n_ex + below(em, lane);
       L.ccomp[rk] = (uint8_t)w_cc(wa[s]);
       L.mcomp[rk] = (uint8_t)w_cm(wa[s]);
@@ -853,28 +1134,82 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     n_w += __popcll(ballot(in && c == WAIT));
   }
   wsync();
-  const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
-  const uint8_t *ccp = L.ccomp, *cmp = L.mcomp;
+  STAMP(11);
+  // the pairwise reductions of the step, one inlined body per source type:
+  //  0,1  sum of the accepted sizes (total_*_requested, env.py:280/285)
+  //  2,3  sum of existing VM sizes (target means, env.py:116-121)
+  //  4,5  sum of PM cpu / memory (ut reward; kl means)
+  //  6,7  PM squared-deviation sums (kl, np.var(cpu/memory))
+  //  8,9  VM-size squared-deviation sums (kl, np.var(vm_cpu/vm_memory[existing]))
+  double *res = L.jobres;
   const double *cent = T.cent;
-  const double sum_c = wave_pw_sum(n_ex, [=](int i) { return cent[ccp[i]]; }, L.pw);
-  const double sum_m = wave_pw_sum(n_ex, [=](int i) { return cent[cmp[i]]; }, L.pw);
-  double tcm = sum_c / (double)P;
+  {  // VM-size sources: accepted sizes, existing sizes, their deviations
+#pragma unroll 1
+    for (int j = (k > 0 ? 0 : 2); j < 4; j++) {
+      const uint8_t *src = (j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp);
+      const int n = j < 2 ? (int)k : n_ex;
+      const double r = wave_pw_sum(n, [=](int i) { return cent[src[i]]; }, L.pw);
+      wsync();
+      if (lane == 0) res[j] = r;
+      wsync();
+    }
+  }
+  if (p.reward >= 1) {  // PM sources (ut, kl)
+    const int jend = p.reward == 2 ? 8 : 6;
+#pragma unroll 1
+    for (int j = 4; j < jend; j++) {
+      const double *src = (j & 1) ? L.mem : L.cpu;
+      const double mean = j < 6 ? 0.0 : res[j - 2] / (double)P;
+      const bool sq = j >= 6;
+      const double r = wave_pw_sum(P, [=](int i) {
+        const double x = src[i];
+        const double d = x - mean;
+        return sq ? d * d : x;
+      }, L.pw);
+      wsync();
+      if (lane == 0) res[j] = r;
+      wsync();
+    }
+  }
+  if (p.reward == 2) {  // VM-size deviations (kl)
+#pragma unroll 1
+    for (int j = 8; j < 10; j++) {
+      const uint8_t *src = (j & 1) ? L.mcomp : L.ccomp;
+      const double mean = res[j - 6] / (double)n_ex;
+      const double r = wave_pw_sum(n_ex, [=](int i) {
+        const double d = cent[src[i]] - mean;
+        return d * d;
+      }, L.pw);
+      wsync();
+      if (lane == 0) res[j] = r;
+      wsync();
+    }
+  }
+  STAMP(12);
+  const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
+  double tcm = res[2] / (double)P;
   if (p.cap_target_util && tcm > 1) tcm = 1.0;
-  double tmm = sum_m / (double)P;
+  double tmm = res[3] / (double)P;
   if (p.cap_target_util && tmm > 1) tmm = 1.0;
   double reward = 0.0;
   if (n_ex > 0) {
-    const double *cpu = L.cpu, *mem = L.mem;
-    if (p.reward == 2) {  // kl
-      reward = kl_block(cpu, mem, P, ccp, cmp, cent, n_ex, sum_c, sum_m, tcm, tmm, L.pw);
-    } else if (p.reward == 1) {  // ut
-      const double sc = wave_pw_sum(P, [=](int i) { return cpu[i]; }, L.pw);
-      const double sm = wave_pw_sum(P, [=](int i) { return mem[i]; }, L.pw);
-      reward = p.beta * sc + (1 - p.beta) * sm;
-    } else {  // wr
+    if (p.reward == 2) {  // kl (env.py:124-149)
+      double cv = res[6] / (double)P, mv = res[7] / (double)P;
+      if (cv == 0) cv = 1e-6;
+      if (mv == 0) mv = 1e-6;
+      double tcv = res[8] / (double)n_ex, tmv = res[9] / (double)n_ex;
+      if (tcv == 0) tcv = 1e-6;
+      if (tmv == 0) tmv = 1e-6;
+      reward = (tcm == 0 || tmm == 0)
+                   ? 0.0
+                   : kl_reward(tcm, tmm, tcv, tmv, res[4] / (double)P, res[5] / (double)P, cv, mv);
+    } else if (p.reward == 1) {  // ut (env.py:150-151)
+      reward = p.beta * res[4] + (1 - p.beta) * res[5];
+    } else {  // wr (env.py:152-153)
       reward = -wr;
     }
   }
+  STAMP(4);
   // ---- counters, termination (env.py:160-163, 101) ----
   const int64_t ts = H->timestep;
   terminated = ts >= p.limit;
@@ -887,6 +1222,10 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     H->waiting_ratio = wr;
     H->tcm = tcm;
     H->tmm = tmm;
+    if (k > 0) {
+      H->total_cpu_req = H->total_cpu_req + res[0];
+      H->total_mem_req = H->total_mem_req + res[1];
+    }
   }
   wsync();
   return reward;
@@ -894,7 +1233,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
 
 template <int VPT>
 __device__ __forceinline__ void write_obs(const EnvParams &p, const Lds &L, const Tables &T,
-                          const uint32_t (&wa)[VPT], float *obs) {
+                                          const uint32_t (&wa)[VPT], float *obs) {
   const int lane = lane_id();
   const int V = p.V, P = p.P;
 #pragma unroll
@@ -915,7 +1254,7 @@ __device__ __forceinline__ void write_obs(const EnvParams &p, const Lds &L, cons
 // get_invalid_action_mask(masked=True) (env.py:45-53), bit-packed, 1 = invalid.
 template <int VPT>
 __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, const Tables &T,
-                           const uint32_t (&wa)[VPT], uint32_t *bits) {
+                                           const uint32_t (&wa)[VPT], uint32_t *bits) {
   const int lane = lane_id();
   const int V = p.V, P = p.P, A = p.A, W = p.W32, WAIT = p.P, NUL = p.P + 1;
 #pragma unroll
@@ -926,6 +1265,7 @@ __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, con
     const double vc = T.cent[w_cc(wa[s])], vm = T.cent[w_cm(wa[s])];
     const bool waiting = in && c == WAIT;
     const bool anyw = ballot(waiting) != 0;
+#pragma unroll 1
     for (int w = 0; w < W; w++) {
       uint32_t word = 0xFFFFFFFFu;
       const int a0 = w * 32;
@@ -933,6 +1273,7 @@ __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, con
       if (c < P && WAIT >= a0 && WAIT < a0 + 32) word &= ~(1u << (WAIT - a0));  // suspend
       if (anyw) {
         const int hi = min(a0 + 32, P);
+#pragma unroll 1
         for (int q = a0; q < hi; q++) {  // uniform q: LDS broadcast reads
           const bool fit = (L.cpu[q] + vc <= 1) && (L.mem[q] + vm <= 1);
           if (waiting && fit) word &= ~(1u << (q - a0));
@@ -947,6 +1288,10 @@ template <int VPT>
 __global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
   extern __shared__ __align__(16) char lds[];
   __shared__ Tables T;
+#ifdef VMP_STAMPS
+  const uint64_t t_start = __builtin_amdgcn_s_memtime();
+  const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int i = threadIdx.x; i < 128; i += blockDim.x) {
     T.cent[i] = (double)i / 100.0;
     T.fcent[i] = (float)((double)i / 100.0);
@@ -957,29 +1302,22 @@ __global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, Step
   const int e = uni(blockIdx.x * kWavesPerBlock + wid);
   if (e >= p.N) return;
   char *base = lds + wid * p.lds_wave_bytes;
-  Lds L;
-  L.hdr = reinterpret_cast<EnvHdr *>(base + p.off_hdr);
-  L.cpu = reinterpret_cast<double *>(base + p.off_pm);
-  L.mem = L.cpu + p.P;
-  L.fcpu = reinterpret_cast<float *>(base + p.off_fpm);
-  L.fmem = L.fcpu + p.P;
-  L.fkey = L.fmem + p.P;
-  L.tc = reinterpret_cast<uint8_t *>(base + p.off_thr);
-  L.tm = L.tc + p.P;
-  L.ord = reinterpret_cast<uint16_t *>(base + p.off_ord);
-  L.bc = reinterpret_cast<uint64_t *>(base + p.off_bits);
-  L.bm = L.bc + 101 * p.NW;
-  L.sortstk = reinterpret_cast<int32_t *>(base + p.off_sort);
-  L.stage = reinterpret_cast<uint64_t *>(base + p.off_stage);
-  L.ccomp = reinterpret_cast<uint8_t *>(base + p.off_ccomp);
-  L.mcomp = L.ccomp + p.V;
-  L.pw.lo = reinterpret_cast<int32_t *>(base + p.off_leaf);
-  L.pw.len = L.pw.lo + p.n_leaf;
-  L.pw.stk = L.pw.len + p.n_leaf;
-  L.pw.acc = reinterpret_cast<double *>(base + p.off_leafval);
-  L.pw.val = L.pw.acc + 8 * p.n_leaf;
+  const Lds L = make_lds(p, base);
   const int V = p.V, P = p.P;
-  // ---- load: VM words to registers, PM resources + header to LDS ----
+  // ---- header and PM resources to LDS; the launch's random draws ----
+  const double *pm = p.pm + (int64_t)e * 2 * P;
+  for (int i = lane; i < 2 * P; i += 64) L.cpu[i] = pm[i];
+  if (lane < 32)
+    reinterpret_cast<uint64_t *>(L.hdr)[lane] = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane];
+  wsync();
+#ifdef VMP_STAMPS
+  const uint64_t t_loaded = __builtin_amdgcn_s_memtime();
+#endif
+  if (o.k_steps > 0) predraw(p, L, o.k_steps, V);
+#ifdef VMP_STAMPS
+  const uint64_t t_drawn = __builtin_amdgcn_s_memtime();
+#endif
+  // ---- VM words to registers ----
   const uint64_t *vmw = p.vmw + (int64_t)e * V;
   uint32_t wa[VPT], rem[VPT];
 #pragma unroll
@@ -989,13 +1327,15 @@ __global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, Step
     wa[s] = (uint32_t)w;
     rem[s] = (uint32_t)(w >> 32);
   }
-  const double *pm = p.pm + (int64_t)e * 2 * P;
-  for (int i = lane; i < 2 * P; i += 64) L.cpu[i] = pm[i];
-  if (lane < 32)
-    reinterpret_cast<uint64_t *>(L.hdr)[lane] = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane];
-  wsync();
+  STAMP_DECL
+#ifdef VMP_STAMPS
+  st_acc[13] = t_loaded - t_start;
+  st_acc[14] = t_drawn - t_loaded;
+  st_acc[15] = st_prev - t_drawn;
+#endif
   bool term = false;
   int64_t ndone = 0;
+#pragma unroll 1
   for (int k = 0; k < o.k_steps; k++) {
     const bool last = k == o.k_steps - 1;
     uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
@@ -1005,27 +1345,33 @@ __global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, Step
       n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row);
     else
       external_apply<VPT>(p, L, T, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
+    STAMP(1);
     wsync();
     if (lane == 0) {
       L.hdr->place_action += n_place;
       L.hdr->suspend_action += n_susp;
     }
     wsync();
-    const double r = env_tail<VPT>(p, L, T, wa, rem, term);
+#ifdef VMP_STAMPS
+    const double r = env_tail<VPT>(p, L, T, wa, rem, k, term, st_acc, st_prev);
+#else
+    const double r = env_tail<VPT>(p, L, T, wa, rem, k, term);
+#endif
     if (o.reward && lane == 0) o.reward[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
+  if (o.k_steps > 0) svc_commit(L);
   if (o.k_steps == 0 && o.policy >= 0 && o.act_out) {
-    // act only: decide on a scratch copy, the state is not stored
+    // act only: decide on a scratch copy of the VM words; nothing is stored
     uint32_t wt[VPT];
 #pragma unroll
     for (int s = 0; s < VPT; s++) wt[s] = wa[s];
     heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr);
-    for (int i = lane; i < 2 * P; i += 64) L.cpu[i] = pm[i];  // undo env events
-    wsync();
   }
+  STAMP(0);
   if (o.obs) write_obs<VPT>(p, L, T, wa, o.obs + (int64_t)e * p.D);
   if (o.mask_bits) write_mask<VPT>(p, L, T, wa, o.mask_bits + (int64_t)e * V * p.W32);
+  STAMP(5);
   if (o.k_steps > 0) {
     if (o.done && lane == 0) o.done[e] = (uint8_t)term;
     if (o.done_count && lane == 0) o.done_count[e] += ndone;
@@ -1040,7 +1386,19 @@ __global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, Step
     if (lane < 32)
       reinterpret_cast<uint64_t *>(p.hdr + e)[lane] = reinterpret_cast<uint64_t *>(L.hdr)[lane];
   }
+  STAMP(6);
+#ifdef VMP_STAMPS
+  st_acc[7] = (__builtin_amdgcn_s_memrealtime() - rt_start) * 1000;  // x1000 (100 MHz ticks)
+  st_acc[9] = __builtin_amdgcn_s_memtime() - t_start;
+#endif
+  STAMP_FLUSH();
 }
+
+template __global__ void k_env<1>(EnvParams, StepOut);
+template __global__ void k_env<2>(EnvParams, StepOut);
+template __global__ void k_env<4>(EnvParams, StepOut);
+template __global__ void k_env<8>(EnvParams, StepOut);
+template __global__ void k_env<16>(EnvParams, StepOut);
 
 // ------------------------------------------------------------- reset -----
 // VmEnv.reset (env.py:180-226) for masked envs, one wave per env.
@@ -1233,11 +1591,5 @@ __global__ __launch_bounds__(256) void k_masked_sample(int B, int V, int A, int 
   }
 }
 
-// Explicit instantiations used by the host dispatcher.
-template __global__ void k_env<1>(EnvParams, StepOut);
-template __global__ void k_env<2>(EnvParams, StepOut);
-template __global__ void k_env<4>(EnvParams, StepOut);
-template __global__ void k_env<8>(EnvParams, StepOut);
-template __global__ void k_env<16>(EnvParams, StepOut);
 
 }  // namespace vmp

@@ -24,6 +24,8 @@ namespace vmp {
 constexpr int kWaveSize = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kMaxVPT = 16;  // VM slots per lane held in registers: V <= 1024
+constexpr int kMaxStepsPerLaunch = 256;  // rollout launches are split by the host
+constexpr int kSpecDraws = 64;           // speculative service draws per launch
 
 struct alignas(16) EnvHdr {
   uint64_t rng[4][4];      // [stream][state_hi, state_lo, inc_hi, inc_lo]; rng1..rng4
@@ -51,8 +53,8 @@ struct EnvParams {
   int64_t limit;          // eval_steps if eval_mode else training_steps
   int64_t M2;             // 2 * max(training_steps, eval_steps)
   double beta, seq_lo, seq_range;
-  PoisConst arr, svc;     // arrivals (rng3), service lengths (rng4)
   const PoisConst *pois;  // device copy: [0] arrivals, [1] service lengths
+  uint64_t *stamps;       // [N][8] phase clocks (diagnostic builds only)
   uint64_t *vmw;
   double *pm;
   EnvHdr *hdr;
@@ -61,7 +63,8 @@ struct EnvParams {
   int32_t NW;      // ceil(P/64) words per fit bitmap row
   int32_t n_leaf;  // capacity of the pairwise-sum leaf list
   int32_t off_hdr, off_pm, off_fpm, off_thr, off_ord, off_bits, off_sort, off_ccomp;
-  int32_t off_leaf, off_leafval, off_stage;
+  int32_t off_leaf, off_leafval, off_stage, off_pre;
+  int32_t scap;    // speculative service draws per launch
 };
 
 struct StepOut {

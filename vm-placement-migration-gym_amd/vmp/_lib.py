@@ -16,7 +16,7 @@ EXPORTS = (
     "vmp_set_eval", "vmp_dims", "vmp_reset", "vmp_step", "vmp_heuristic_act",
     "vmp_heuristic_step", "vmp_rollout_heuristic", "vmp_mask", "vmp_mask_bool", "vmp_get_obs",
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
-    "vmp_masked_sample",
+    "vmp_masked_sample", "vmp_debug_stamps",
 )
 
 
@@ -83,6 +83,7 @@ def lib():
         "vmp_get_rank": (ctypes.c_int, [P, P]),
         "vmp_gae": (ctypes.c_int, [i32, i32, P, P, P, P, f32, f32, P, P, P]),
         "vmp_masked_sample": (ctypes.c_int, [i32, i32, i32, P, P, u64, u64, P, P, P, P]),
+        "vmp_debug_stamps": (ctypes.c_int, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
