@@ -201,7 +201,7 @@ def main():
                    "parallelism": f"env-shard x{world}", "steady_state_ff_steps": args.ff_steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_env<16> (heuristic act+step)", "kernel_ms": kern_ms,
+                     "kernel": "vmp::k_env<16, true> (heuristic act+step, one step per launch)", "kernel_ms": kern_ms,
                      "bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},

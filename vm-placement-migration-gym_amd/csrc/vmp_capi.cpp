@@ -14,7 +14,7 @@
 #include "vmp_layout.h"
 
 namespace vmp {
-template <int VPT>
+template <int VPT, bool ONE>
 __global__ void k_env(EnvParams p, StepOut o);
 __global__ void k_reset(EnvParams p, const int64_t *seeds, const uint8_t *env_mask, float *obs);
 __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double *vm_mem,
@@ -180,6 +180,16 @@ void carve(vmp_handle *h) {
   p.lds_wave_bytes = (int32_t)off;
 }
 
+template <bool ONE>
+void launch_vpt(int need, dim3 grid, dim3 block, size_t lds, hipStream_t s, const EnvParams &p,
+                const StepOut &o) {
+  if (need <= 1) hipLaunchKernelGGL((k_env<1, ONE>), grid, block, lds, s, p, o);
+  else if (need <= 2) hipLaunchKernelGGL((k_env<2, ONE>), grid, block, lds, s, p, o);
+  else if (need <= 4) hipLaunchKernelGGL((k_env<4, ONE>), grid, block, lds, s, p, o);
+  else if (need <= 8) hipLaunchKernelGGL((k_env<8, ONE>), grid, block, lds, s, p, o);
+  else hipLaunchKernelGGL((k_env<16, ONE>), grid, block, lds, s, p, o);
+}
+
 int launch_env(vmp_handle *h, const StepOut &o) {
   dim3 grid((h->N + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
   EnvParams p = h->prm;
@@ -190,11 +200,8 @@ int launch_env(vmp_handle *h, const StepOut &o) {
   size_t lds = (size_t)p.lds_wave_bytes * kWavesPerBlock;
   if (lds > 160 * 1024 - 2048) return fail(VMP_EINVAL, "config too large for the LDS carve");
   const int need = (h->V + 63) / 64;
-  if (need <= 1) hipLaunchKernelGGL(k_env<1>, grid, block, lds, h->stream, p, o);
-  else if (need <= 2) hipLaunchKernelGGL(k_env<2>, grid, block, lds, h->stream, p, o);
-  else if (need <= 4) hipLaunchKernelGGL(k_env<4>, grid, block, lds, h->stream, p, o);
-  else if (need <= 8) hipLaunchKernelGGL(k_env<8>, grid, block, lds, h->stream, p, o);
-  else hipLaunchKernelGGL(k_env<16>, grid, block, lds, h->stream, p, o);
+  if (o.k_steps == 1) launch_vpt<true>(need, grid, block, lds, h->stream, p, o);
+  else launch_vpt<false>(need, grid, block, lds, h->stream, p, o);
   HIP_TRY(hipGetLastError());
   return VMP_OK;
 }

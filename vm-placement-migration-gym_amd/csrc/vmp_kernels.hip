@@ -21,6 +21,9 @@
 #ifndef VMP_WAVES_PER_EU
 #define VMP_WAVES_PER_EU 2
 #endif
+#ifndef VMP_WAVES_PER_EU_ONE  // the per-step (k_steps == 1) instantiation
+#define VMP_WAVES_PER_EU_ONE 2
+#endif
 
 namespace vmp {
 
@@ -1284,8 +1287,10 @@ __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, con
   }
 }
 
-template <int VPT>
-__global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
+// ONE = true is the per-step launch (k_steps == 1, the Base.test loop body); it
+// is a separate instantiation so profiles tell it apart from fused rollouts.
+template <int VPT, bool ONE>
+__global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
   extern __shared__ __align__(16) char lds[];
   __shared__ Tables T;
 #ifdef VMP_STAMPS
@@ -1335,9 +1340,10 @@ __global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, Step
 #endif
   bool term = false;
   int64_t ndone = 0;
+  const int k_steps = ONE ? 1 : o.k_steps;
 #pragma unroll 1
-  for (int k = 0; k < o.k_steps; k++) {
-    const bool last = k == o.k_steps - 1;
+  for (int k = 0; k < k_steps; k++) {
+    const bool last = k == k_steps - 1;
     uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
     int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
     int64_t n_place = 0, n_susp = 0;
@@ -1394,11 +1400,16 @@ __global__ __launch_bounds__(256, VMP_WAVES_PER_EU) void k_env(EnvParams p, Step
   STAMP_FLUSH();
 }
 
-template __global__ void k_env<1>(EnvParams, StepOut);
-template __global__ void k_env<2>(EnvParams, StepOut);
-template __global__ void k_env<4>(EnvParams, StepOut);
-template __global__ void k_env<8>(EnvParams, StepOut);
-template __global__ void k_env<16>(EnvParams, StepOut);
+template __global__ void k_env<1, false>(EnvParams, StepOut);
+template __global__ void k_env<1, true>(EnvParams, StepOut);
+template __global__ void k_env<2, false>(EnvParams, StepOut);
+template __global__ void k_env<2, true>(EnvParams, StepOut);
+template __global__ void k_env<4, false>(EnvParams, StepOut);
+template __global__ void k_env<4, true>(EnvParams, StepOut);
+template __global__ void k_env<8, false>(EnvParams, StepOut);
+template __global__ void k_env<8, true>(EnvParams, StepOut);
+template __global__ void k_env<16, false>(EnvParams, StepOut);
+template __global__ void k_env<16, true>(EnvParams, StepOut);
 
 // ------------------------------------------------------------- reset -----
 // VmEnv.reset (env.py:180-226) for masked envs, one wave per env.
