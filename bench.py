@@ -3,8 +3,9 @@
 Workload (BASELINE.json north_star, SURVEY §8(d) C-main): config/100.yml with
 vms=1000 (P100 V1000, arrival_rate 1.8182 as shipped, service_length 1000,
 reward wr, allow_null_action), FirstFit act + VmEnv.step fused in one launch per
-step for every env (the Base.test loop body, base.py:71-86), obs/reward/done
-written to HBM each step. Envs per GPU fixed (weak scaling); env i of the job
+step for every env (the Base.test loop body, base.py:71-86) in training mode
+(info = {} as in env.py:168; the eval-mode info metrics are derived on demand
+by vmp_get_stats), obs/reward/done written to HBM each step. Envs per GPU fixed (weak scaling); env i of the job
 has seed 4*i. Before timing, every env is fast-forwarded to the
 steady-state fill (~200 running / ~800 waiting VMs) with the fused rollout.
 
@@ -75,7 +76,7 @@ def main():
     D = 3 * V + 2 * P
     seeds = 4 * (rank * N + np.arange(N, dtype=np.int64))
     env = BatchedVmEnv(Config(**CFG), N, seeds=seeds, device=dev)
-    env.eval(True)
+    env.eval(False)
     L = _lib.lib()
     stream = torch.cuda.current_stream(dev)
     h = env._bind()
@@ -158,7 +159,7 @@ def main():
         errs, ctr_ok = [], True
         for i in range(n_chk):
             e = O.OracleEnv(dict(CFG, seed=int(seeds[i])))
-            e.eval(True)
+            e.eval(False)
             e.reset(int(seeds[i]))
             for s in range(steps_done - kr):
                 e.step(e.firstfit())
@@ -197,7 +198,7 @@ def main():
                                "VmEnv.step fused, one launch per step", "envs_per_gpu": N,
                    "global_envs": world * N, "pms": P, "vms": V,
                    "arrival_rate": CFG["arrival_rate"], "service_length": CFG["service_length"],
-                   "reward_function": "wr", "policy": "firstfit",
+                   "reward_function": "wr", "policy": "firstfit", "mode": "train",
                    "parallelism": f"env-shard x{world}", "steady_state_ff_steps": args.ff_steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -170,7 +170,7 @@ int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
                       int32_t *action, float *logprob, float *entropy, void *hip_stream);
 
 /* Diagnostics: per-env shader-clock cycles per kernel phase, accumulated since
- * the previous call, device u64[n_env][16] (see tools/stamps.py for the phase names).
+ * the previous call, device u64[n_env][24] (see tools/stamps.py for the phase names).
  * Only a library built with -DVMP_STAMPS records them; otherwise
  * returns VMP_EINVAL. */
 int vmp_debug_stamps(vmp_handle *h, uint64_t *out);

@@ -17,10 +17,11 @@ V = int(sys.argv[2]) if len(sys.argv) > 2 else 1000
 cfg = Config(pms=100, vms=V, arrival_rate=1.8182, service_length=1000, training_steps=10000,
              eval_steps=100000, seed=0, reward_function="wr", allow_null_action=True)
 env = BatchedVmEnv(cfg, N)
-env.eval(True)
+env.eval(os.environ.get("STAMP_TRAIN") is None)
 for _ in range(25):
     env.rollout("firstfit", 100)
-buf = torch.zeros((N, 16), dtype=torch.int64, device="cuda")
+NS = 24
+buf = torch.zeros((N, NS), dtype=torch.int64, device="cuda")
 _lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
 K = 50
 for _ in range(K):
@@ -30,12 +31,13 @@ _lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
 torch.cuda.synchronize()
 st = buf.cpu().numpy().astype(np.float64) / K
 names = ["loop-end", "act+apply(rest)", "run_vms", "accept", "stats(rest)+reward", "obs", "store",
-         "-", "heur:prep", "heur:bitmaps", "heur:resolve", "stats:compress", "stats:pw-sums",
-         "pro:start->hdr/pm loaded", "pro:predraw", "pro:VM words loaded"]
-tot = st[:, :16].sum(1) - st[:, 7] - st[:, 9]
+         "-", "-", "-", "-", "stats:compress", "stats:pw-sums",
+         "pro:start->hdr/pm loaded", "pro:predraw", "pro:VM words loaded",
+         "heur:prep", "heur:bitmaps", "heur:queries", "heur:apply", "-", "-", "-", "-"]
+tot = st.sum(1) - st[:, 7] - st[:, 9]
 print(f"N={N} V={V}: mean cycles per env-step (per wave) = {tot.mean():.0f}")
-for i in range(16):
-    if names[i] != "-" and i not in (7, 9):
+for i in range(NS):
+    if names[i] != "-":
         print(f"  {names[i]:20s} {st[:, i].mean():10.0f}  ({100 * st[:, i].mean() / tot.mean():5.1f}%)")
 ctr = env.counters().cpu().numpy()
 pl = env.state()["vm_placement"].cpu().numpy()

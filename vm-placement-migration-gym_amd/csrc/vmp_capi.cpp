@@ -14,12 +14,14 @@
 #include "vmp_layout.h"
 
 namespace vmp {
+constexpr int kStamps = 24;  // per-env phase clocks (diagnostic builds)
 template <int VPT, bool ONE>
 __global__ void k_env(EnvParams p, StepOut o);
 __global__ void k_reset(EnvParams p, const int64_t *seeds, const uint8_t *env_mask, float *obs);
 __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double *vm_mem,
                          double *cpu, double *mem, int64_t *remaining, int64_t *rank);
 __global__ void k_counters(EnvParams p, int64_t *ctr, double *st);
+__global__ void k_target_means(EnvParams p);
 __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, uint8_t *mask);
 __global__ void k_gae(int T, int N, const float *r, const float *d, const float *v,
                       const float *nv, float gamma, float lam, float *adv, float *ret);
@@ -291,8 +293,8 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   p.hdr = h->hdr;
   carve(h);
 #ifdef VMP_STAMPS
-  HIP_TRY(hipMalloc(&h->stamps, sizeof(uint64_t) * 16 * (size_t)n_env));
-  HIP_TRY(hipMemset(h->stamps, 0, sizeof(uint64_t) * 16 * (size_t)n_env));
+  HIP_TRY(hipMalloc(&h->stamps, sizeof(uint64_t) * kStamps * (size_t)n_env));
+  HIP_TRY(hipMemset(h->stamps, 0, sizeof(uint64_t) * kStamps * (size_t)n_env));
   p.stamps = h->stamps;
 #endif
   int maxn = h->V > h->P ? h->V : h->P;
@@ -461,6 +463,8 @@ int vmp_get_counters(vmp_handle *h, int64_t *counters) {
 
 int vmp_get_stats(vmp_handle *h, double *stats) {
   if (!h || !stats) return fail(VMP_EINVAL, "null argument");
+  hipLaunchKernelGGL(k_target_means, dim3((h->N + kWavesPerBlock - 1) / kWavesPerBlock),
+                     dim3(64 * kWavesPerBlock), 0, h->stream, h->prm);
   hipLaunchKernelGGL(k_counters, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,
                      nullptr, stats);
   HIP_TRY(hipGetLastError());
@@ -515,9 +519,9 @@ int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
 int vmp_debug_stamps(vmp_handle *h, uint64_t *out) {
   if (!h || !out) return fail(VMP_EINVAL, "null argument");
   if (!h->stamps) return fail(VMP_EINVAL, "library built without -DVMP_STAMPS");
-  HIP_TRY(hipMemcpyAsync(out, h->stamps, sizeof(uint64_t) * 16 * (size_t)h->N,
+  HIP_TRY(hipMemcpyAsync(out, h->stamps, sizeof(uint64_t) * kStamps * (size_t)h->N,
                          hipMemcpyDeviceToDevice, h->stream));
-  HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(uint64_t) * 16 * (size_t)h->N, h->stream));
+  HIP_TRY(hipMemsetAsync(h->stamps, 0, sizeof(uint64_t) * kStamps * (size_t)h->N, h->stream));
   return VMP_OK;
 }
 

@@ -16,6 +16,11 @@
 
 #include "vmp_layout.h"
 
+// Pointers into LDS carry address space 3 explicitly: 32-bit addresses (half
+// the SGPRs of generic pointers) and ds_* instructions without relying on
+// address-space inference through the helpers.
+#define LDSP __attribute__((address_space(3)))
+
 // Minimum waves per SIMD the env kernel is register-allocated for
 // (__launch_bounds__ 2nd argument); measured choice, see DESIGN.md.
 #ifndef VMP_WAVES_PER_EU
@@ -201,28 +206,13 @@ __device__ __forceinline__ int64_t poisson(Pcg &r, const PoisConst &c) {
   }
 }
 
-// Out of line: one Poisson draw from stream k of the wave's LDS header (all
-// lanes call it with identical state; lane 0 writes the advanced state back).
-__device__ __forceinline__ int64_t poisson_lds(uint64_t *hdr_rng, const PoisConst *c) {
-  Pcg r;
-  r.s = U128{hdr_rng[0], hdr_rng[1]};
-  r.inc = U128{hdr_rng[2], hdr_rng[3]};
-  const int64_t x = poisson(r, *c);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if ((threadIdx.x & 63) == 0) {
-    hdr_rng[0] = r.s.hi;
-    hdr_rng[1] = r.s.lo;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  return x;
-}
-
 // Diagnostic build only (-DVMP_STAMPS): per-phase shader-clock deltas,
-// accumulated per env into p.stamps[e][8]. No stamp executes otherwise.
+// accumulated per env into p.stamps[e][kStamps]. No stamp executes otherwise.
 #ifdef VMP_STAMPS
-#define STAMP_DECL uint64_t st_acc[16] = {0}, st_prev = __builtin_amdgcn_s_memtime();
+constexpr int kStamps = 24;
+#define STAMP_PARAMS , uint64_t (&st_acc)[kStamps], uint64_t &st_prev
+#define STAMP_ARGS , st_acc, st_prev
+#define STAMP_DECL uint64_t st_acc[kStamps] = {0}, st_prev = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                   \
   do {                                             \
     const uint64_t _t = __builtin_amdgcn_s_memtime(); \
@@ -232,9 +222,11 @@ __device__ __forceinline__ int64_t poisson_lds(uint64_t *hdr_rng, const PoisCons
 #define STAMP_FLUSH()                                                         \
   do {                                                                        \
     if (p.stamps && lane == 0)                                                \
-      for (int _i = 0; _i < 16; _i++) p.stamps[(int64_t)e * 16 + _i] += st_acc[_i]; \
+      for (int _i = 0; _i < kStamps; _i++) p.stamps[(int64_t)e * kStamps + _i] += st_acc[_i]; \
   } while (0)
 #else
+#define STAMP_PARAMS
+#define STAMP_ARGS
 #define STAMP_DECL
 #define STAMP(i)
 #define STAMP_FLUSH()
@@ -248,10 +240,10 @@ __device__ __forceinline__ int64_t poisson_lds(uint64_t *hdr_rng, const PoisCons
 // enumerated and the partial sums combined by lane 0 alone on small LDS
 // stacks, so no cross-lane hand-off happens inside the recursion.
 struct PwLds {
-  int32_t *lo, *len;  // leaf list (DFS order), n_leaf entries
-  int32_t *stk;       // lane-0 stack, 3 * 64 ints
-  double *acc;        // 8 accumulators per leaf
-  double *val;        // leaf sums, + value stack
+  int32_t LDSP *lo, *len;  // leaf list (DFS order), n_leaf entries
+  int32_t LDSP *stk;            // lane-0 stack, 3 * 64 ints
+  double LDSP *acc;             // 8 accumulators per leaf
+  double LDSP *val;             // leaf sums, + value stack
 };
 
 // lane 0 only: leaves of the recursion for n, left to right.
@@ -282,7 +274,7 @@ __device__ __forceinline__ int pw_plan(int n, const PwLds &S) {
 
 // lane 0 only: pw(n) = pw(n2) + pw(n - n2) over the leaf sums in val[].
 __device__ __forceinline__ double pw_combine(int n, const PwLds &S, int nl) {
-  double *vs = S.val + nl;  // value stack after the leaf sums
+  double LDSP *vs = S.val + nl;  // value stack after the leaf sums
   int sp = 0, vsp = 0, leaf = 0;
   S.stk[0] = n;
   S.stk[1] = 0;
@@ -390,6 +382,12 @@ __device__ __forceinline__ double pw_leaf_group(int o, int m, F &f) {
 template <class F>
 __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
   const int lane = lane_id();
+  if (n < 8) {  // pairwise_sum's direct loop, evaluated by every lane alike
+    double r = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < n; i++) r += f(i);
+    return r;
+  }
   if (n <= 128) return readlane_f64(pw_leaf_group(0, n, f), 0);
   if (n <= 1928) {
     int my_o = 0, my_m = 0, nl = 0;
@@ -424,33 +422,13 @@ __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
   return r;
 }
 
-// The reductions of one step, through ONE out-of-line body: x(i) is
-// cent[u8[i]] (VM sizes) or f64[i] (PM resources), optionally (x - mean)^2.
-enum PwKind { PW_U8 = 0, PW_F64 = 1, PW_U8_SQDEV = 2, PW_F64_SQDEV = 3 };
-__device__ __forceinline__ double pw_sum(int n, int kind, const void *src, const double *cent,
-                                         double mean, PwLds S) {
-  const uint8_t *u8 = (const uint8_t *)src;
-  const double *f64 = (const double *)src;
-  return wave_pw_sum(
-      n,
-      [=](int i) {
-        double x = (kind & 1) ? f64[i] : cent[u8[i]];
-        if (kind & 2) {
-          const double d = x - mean;
-          x = d * d;
-        }
-        return x;
-      },
-      S);
-}
-
 // ------------------------------------------- numpy scalar argsort (BF) ----
 // aquicksort_<float_tag> / aheapsort_ (npysort), run by ONE lane on LDS
 // arrays (index form of the pointer algorithm); stack arrays live in LDS.
 __device__ __forceinline__ bool fless(float a, float b) { return a < b || (b != b && a == a); }
 
-__device__ void aheapsort_lds(const float *v, uint16_t *tosort, int n) {
-  uint16_t *a = tosort - 1;
+__device__ void aheapsort_lds(const float LDSP *v, uint16_t LDSP *tosort, int n) {
+  uint16_t LDSP *a = tosort - 1;
   int i, j, l;
   uint16_t tmp;
   for (l = n >> 1; l > 0; --l) {
@@ -483,8 +461,9 @@ __device__ void aheapsort_lds(const float *v, uint16_t *tosort, int n) {
   }
 }
 
-__device__ __noinline__ void aquicksort_lds(const float *v, uint16_t *t, int num, int32_t *stack) {
-  int32_t *depth = stack + 128;
+__device__ __noinline__ void aquicksort_lds(const float LDSP *v, uint16_t LDSP *t, int num,
+                                            int32_t LDSP *stack) {
+  int32_t LDSP *depth = stack + 128;
   int pl = 0, pr = num - 1;
   int sp = 0, dp = 0;
   int cdepth = 0;
@@ -541,58 +520,58 @@ __device__ __noinline__ void aquicksort_lds(const float *v, uint16_t *t, int num
 // --------------------------------------------------------- env kernel ----
 // Per-wave LDS carve (offsets from EnvParams, computed by the host).
 struct Lds {
-  EnvHdr *hdr;             // the env's 256-B header (scalars, RNG streams)
-  double *cpu, *mem;       // f64[P] PM resources (the env state)
-  float *fcpu, *fmem;      // f32[P] observation view used by the heuristics
-  float *fkey;             // BF keys fcpu + fmem
-  uint8_t *tc, *tm;        // per-PM largest fitting size (hundredths), f32 semantics
-  uint16_t *ord;           // BF ascending argsort, then reversed into visiting order
-  uint64_t *bc, *bm;       // [101][NW] fit bitmaps by size (bit = visiting position)
-  int32_t *sortstk;        // introsort stacks
-  uint16_t *nulls;         // NULL slot indices (aliases the fit bitmaps)
-  uint8_t *accc, *accm;    // accepted sizes (alias the fit bitmaps)
-  double *jobres;          // reduction results of the step
-  int32_t *arr;            // per-step arrivals of the launch (prologue draws)
-  uint32_t *svc;           // speculative planned runtimes
-  uint64_t *svcst;         // rng4 state after each speculative draw
-  uint64_t *svcfb;         // rng4 state for fallback draws
-  int32_t *svcinfo;        // [0] speculative count, [1] consumed
-  uint8_t *ccomp, *mcomp;  // compressed sizes of existing VMs [V]
+  EnvHdr LDSP *hdr;                  // the env's 256-B header (scalars, RNG streams)
+  double LDSP *cpu, *mem;       // f64[P] PM resources (the env state)
+  float LDSP *fcpu, *fmem;      // f32[P] observation view used by the heuristics
+  float LDSP *fkey;                  // BF keys fcpu + fmem
+  uint8_t LDSP *tc, *tm;        // per-PM largest fitting size (hundredths), f32 semantics
+  uint16_t LDSP *ord;                // BF ascending argsort, then reversed into visiting order
+  uint64_t LDSP *bc, *bm;       // [101][NW] fit bitmaps by size (bit = visiting position)
+  int32_t LDSP *sortstk;             // introsort stacks
+  uint16_t LDSP *nulls;              // NULL slot indices (aliases the fit bitmaps)
+  uint8_t LDSP *accc, *accm;    // accepted sizes (alias the fit bitmaps)
+  double LDSP *jobres;               // reduction results of the step
+  int32_t LDSP *arr;                 // per-step arrivals of the launch (prologue draws)
+  uint32_t LDSP *svc;                // speculative planned runtimes
+  uint64_t LDSP *svcst;              // rng4 state after each speculative draw
+  uint64_t LDSP *svcfb;              // rng4 state for fallback draws
+  int32_t LDSP *svcinfo;             // [0] speculative count, [1] consumed
+  uint8_t LDSP *ccomp, *mcomp;  // compressed sizes of existing VMs [V]
   PwLds pw;
-  char *base;              // the wave's LDS region
+  char LDSP *base;                   // the wave's LDS region
 };
 
 // The wave's LDS view, rebuilt from its base address (cheap; avoids passing
 // the pointer struct by value into out-of-line helpers).
-__device__ __forceinline__ Lds make_lds(const EnvParams &p, char *base) {
+__device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   Lds L;
-  L.hdr = reinterpret_cast<EnvHdr *>(base + p.off_hdr);
-  L.cpu = reinterpret_cast<double *>(base + p.off_pm);
+  L.hdr = reinterpret_cast<EnvHdr LDSP *>(base + p.off_hdr);
+  L.cpu = reinterpret_cast<double LDSP *>(base + p.off_pm);
   L.mem = L.cpu + p.P;
-  L.fcpu = reinterpret_cast<float *>(base + p.off_fpm);
+  L.fcpu = reinterpret_cast<float LDSP *>(base + p.off_fpm);
   L.fmem = L.fcpu + p.P;
   L.fkey = L.fmem + p.P;
-  L.tc = reinterpret_cast<uint8_t *>(base + p.off_thr);
+  L.tc = reinterpret_cast<uint8_t LDSP *>(base + p.off_thr);
   L.tm = L.tc + p.P;
-  L.ord = reinterpret_cast<uint16_t *>(base + p.off_ord);
-  L.bc = reinterpret_cast<uint64_t *>(base + p.off_bits);
+  L.ord = reinterpret_cast<uint16_t LDSP *>(base + p.off_ord);
+  L.bc = reinterpret_cast<uint64_t LDSP *>(base + p.off_bits);
   L.bm = L.bc + 101 * p.NW;
-  L.sortstk = reinterpret_cast<int32_t *>(base + p.off_sort);
-  L.nulls = reinterpret_cast<uint16_t *>(base + p.off_bits);
-  L.accc = reinterpret_cast<uint8_t *>(base + p.off_bits) + 2 * p.V;
+  L.sortstk = reinterpret_cast<int32_t LDSP *>(base + p.off_sort);
+  L.nulls = reinterpret_cast<uint16_t LDSP *>(base + p.off_bits);
+  L.accc = reinterpret_cast<uint8_t LDSP *>(base + p.off_bits) + 2 * p.V;
   L.accm = L.accc + p.V;
-  L.jobres = reinterpret_cast<double *>(base + p.off_stage);
-  L.svcinfo = reinterpret_cast<int32_t *>(base + p.off_stage + 8 * 12);
-  L.svcfb = reinterpret_cast<uint64_t *>(base + p.off_stage + 8 * 14);
-  L.svcst = reinterpret_cast<uint64_t *>(base + p.off_pre);
-  L.svc = reinterpret_cast<uint32_t *>(base + p.off_pre + 16 * p.scap);
-  L.arr = reinterpret_cast<int32_t *>(base + p.off_pre + 20 * p.scap);
-  L.ccomp = reinterpret_cast<uint8_t *>(base + p.off_ccomp);
+  L.jobres = reinterpret_cast<double LDSP *>(base + p.off_stage);
+  L.svcinfo = reinterpret_cast<int32_t LDSP *>(base + p.off_stage + 8 * 12);
+  L.svcfb = reinterpret_cast<uint64_t LDSP *>(base + p.off_stage + 8 * 14);
+  L.svcst = reinterpret_cast<uint64_t LDSP *>(base + p.off_pre);
+  L.svc = reinterpret_cast<uint32_t LDSP *>(base + p.off_pre + 16 * p.scap);
+  L.arr = reinterpret_cast<int32_t LDSP *>(base + p.off_pre + 20 * p.scap);
+  L.ccomp = reinterpret_cast<uint8_t LDSP *>(base + p.off_ccomp);
   L.mcomp = L.ccomp + p.V;
-  L.pw.lo = reinterpret_cast<int32_t *>(base + p.off_leaf);
+  L.pw.lo = reinterpret_cast<int32_t LDSP *>(base + p.off_leaf);
   L.pw.len = L.pw.lo + p.n_leaf;
   L.pw.stk = L.pw.len + p.n_leaf;
-  L.pw.acc = reinterpret_cast<double *>(base + p.off_leafval);
+  L.pw.acc = reinterpret_cast<double LDSP *>(base + p.off_leafval);
   L.pw.val = L.pw.acc + 8 * p.n_leaf;
   L.base = base;
   return L;
@@ -605,62 +584,75 @@ struct Tables {
 };
 
 __device__ __forceinline__ int w_pl(uint32_t w) { return (int)(w & 0xFFFFu); }
+// Register slots past V hold placement kPad: no test for running (< P), WAIT,
+// NULL or existing (<= WAIT) matches it, so the per-slot loops need no lane
+// range mask (keeping 16 64-bit masks live would spill SGPRs); only stores
+// test live().
+constexpr int kPad = 0xFFFF;
+__device__ __forceinline__ bool live(uint32_t w) { return w_pl(w) != kPad; }
 __device__ __forceinline__ int w_cc(uint32_t w) { return (int)((w >> 16) & 0xFFu); }
 __device__ __forceinline__ int w_cm(uint32_t w) { return (int)(w >> 24); }
 __device__ __forceinline__ uint32_t w_make(int pl, int cc, int cm) {
   return (uint32_t)pl | ((uint32_t)cc << 16) | ((uint32_t)cm << 24);
 }
 
-__device__ __forceinline__ Pcg ld_pcg(const EnvHdr *h, int k) {
+__device__ __forceinline__ Pcg ld_pcg(const EnvHdr LDSP *h, int k) {
   Pcg r;
   r.s = U128{h->rng[k][0], h->rng[k][1]};
   r.inc = U128{h->rng[k][2], h->rng[k][3]};
   return r;
 }
-__device__ __forceinline__ void st_pcg(EnvHdr *h, int k, const Pcg &r) {
+__device__ __forceinline__ void st_pcg(EnvHdr LDSP *h, int k, const Pcg &r) {
   if (lane_id() == 0) {
     h->rng[k][0] = r.s.hi;
     h->rng[k][1] = r.s.lo;
   }
 }
 
-// Largest k in [0, 100] with f + FC[k] <= 1 in f32 (monotone in k), or -1:
-// start from the estimate (1-f)*100 and walk (almost always 0-1 steps).
-__device__ __forceinline__ int fit_threshold(float f, const float *fc) {
-  int k = (int)((1.0f - f) * 100.0f);
-  k = k < 0 ? 0 : (k > 100 ? 100 : k);
-  if (f + fc[k] <= 1.0f) {
-#pragma unroll 1
-    while (k < 100 && f + fc[k + 1] <= 1.0f) k++;
-    return k;
-  }
-#pragma unroll 1
-  while (k > 0 && !(f + fc[k - 1] <= 1.0f)) k--;
-  return k - 1;
+// FC(k) = (float)(k / 100.0), the f32 obs value of a size of k hundredths;
+// (float)(k * 0.01) equals it for every k in [0, 127] (checked exhaustively).
+__device__ __forceinline__ float fcent_of(int k) { return (float)((double)k * 0.01); }
+
+// Largest k in [0, 100] with f + FC(k) <= 1 in f32 (monotone in k), or -1.
+// For every f32 f in [0, 1] (PM loads, env.py:267-268 keeps them >= 0) the
+// answer is one of k0 - 1, k0, k0 + 1 with k0 = (int)((1 - f) * 100): checked
+// exhaustively over all 1 065 353 217 such f.
+__device__ __forceinline__ int fit_threshold(float f) {
+  int k0 = (int)((1.0f - f) * 100.0f);
+  k0 = k0 < 0 ? 0 : (k0 > 100 ? 100 : k0);
+  const bool up = k0 < 100 && f + fcent_of(k0 + 1) <= 1.0f;
+  const bool at = f + fcent_of(k0) <= 1.0f;
+  return up ? k0 + 1 : (at ? k0 : k0 - 1);
 }
 
-__device__ __forceinline__ uint64_t shfl_down_u64(uint64_t x, int d) {
-  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)x, d);
-  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(x >> 32), d);
-  return ((uint64_t)hi << 32) | lo;
-}
-// Suffix OR across the wave: lane k gets OR of x over lanes >= k.
-__device__ __forceinline__ uint64_t suffix_or(uint64_t x) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = shfl_down_u64(x, d);
-    if (lane + d < 64) x |= y;
-  }
+// Inclusive prefix OR across the wave (lane i: OR of lanes 0..i) with DPP row
+// shifts and the GFX9 row broadcasts: 6 VALU steps, no LDS traffic.
+__device__ __forceinline__ uint32_t prefix_or32(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return x;
+}
+__device__ __forceinline__ uint64_t prefix_or64(uint64_t x) {
+  return ((uint64_t)prefix_or32((uint32_t)(x >> 32)) << 32) | prefix_or32((uint32_t)x);
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // Rebuild the fit bitmaps: bit i of bc[k][w] is set iff the PM at visiting
 // position w*64+i accepts a VM of cpu size k/100 (f32 obs arithmetic), i.e.
 // iff its threshold tc >= k. PMs are bucketed by threshold with LDS atomic
-// ORs, then a suffix OR over k (lanes) turns buckets into "tc >= k" masks.
-__device__ __forceinline__ void build_bitmaps(const EnvParams &p, char *lbase, bool bf) {
-  const Lds L = make_lds(p, lbase);
+// ORs, then an OR-scan over k turns buckets into "tc >= k" masks. Rows are
+// mapped to lanes in reverse (row 63-i, and row 127-i for rows 64..100) so
+// the suffix over k is a DPP prefix scan over lanes.
+__device__ __forceinline__ void build_bitmaps(const EnvParams &p, const Lds &L, bool bf) {
   const int lane = lane_id();
   const int P = p.P, NW = p.NW;
   for (int i = lane; i < 101 * NW; i += 64) {
@@ -673,26 +665,25 @@ __device__ __forceinline__ void build_bitmaps(const EnvParams &p, char *lbase, b
     if (pos < P) {
       const int q = bf ? (int)L.ord[pos] : pos;
       const int tcq = (int)L.tc[q] - 1, tmq = (int)L.tm[q] - 1;
-      if (tcq >= 0) atomicOr((unsigned long long *)&L.bc[tcq * NW + w], 1ull << lane);
-      if (tmq >= 0) atomicOr((unsigned long long *)&L.bm[tmq * NW + w], 1ull << lane);
+      if (tcq >= 0) __atomic_fetch_or(&L.bc[tcq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
+      if (tmq >= 0) __atomic_fetch_or(&L.bm[tmq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
     }
   }
   wsync();
+  const int rlo = 63 - lane, rhi = 127 - lane;
+  const bool hi_ok = rhi <= 100;
   for (int w = 0; w < NW; w++) {
-    const bool hi_ok = lane + 64 < 101;
-    uint64_t c1 = hi_ok ? L.bc[(lane + 64) * NW + w] : 0, m1 = hi_ok ? L.bm[(lane + 64) * NW + w] : 0;
-    uint64_t c0 = L.bc[lane * NW + w], m0 = L.bm[lane * NW + w];
-    c1 = suffix_or(c1);
-    m1 = suffix_or(m1);
-    const uint64_t ct = (uint64_t)__shfl((long long)c1, 0), mt = (uint64_t)__shfl((long long)m1, 0);
-    c0 = suffix_or(c0) | ct;
-    m0 = suffix_or(m0) | mt;
-    wsync();
-    L.bc[lane * NW + w] = c0;
-    L.bm[lane * NW + w] = m0;
+    uint64_t c1 = hi_ok ? L.bc[rhi * NW + w] : 0, m1 = hi_ok ? L.bm[rhi * NW + w] : 0;
+    uint64_t c0 = L.bc[rlo * NW + w], m0 = L.bm[rlo * NW + w];
+    c1 = prefix_or64(c1);
+    m1 = prefix_or64(m1);
+    c0 = prefix_or64(c0) | readlane_u64(c1, 63);
+    m0 = prefix_or64(m0) | readlane_u64(m1, 63);
+    L.bc[rlo * NW + w] = c0;
+    L.bm[rlo * NW + w] = m0;
     if (hi_ok) {
-      L.bc[(lane + 64) * NW + w] = c1;
-      L.bm[(lane + 64) * NW + w] = m1;
+      L.bc[rhi * NW + w] = c1;
+      L.bm[rhi * NW + w] = m1;
     }
   }
   wsync();
@@ -713,8 +704,7 @@ __device__ __forceinline__ int bm_query(const Lds &L, int NW, int kc, int km) {
   return -1;
 }
 
-__device__ __forceinline__ void bf_sort(const EnvParams &p, char *lbase) {
-  const Lds L = make_lds(p, lbase);
+__device__ __forceinline__ void bf_sort(const EnvParams &p, const Lds &L) {
   const int lane = lane_id();
   const int P = p.P;
   for (int i = lane; i < P; i += 64) L.fkey[i] = L.fcpu[i] + L.fmem[i];
@@ -747,12 +737,6 @@ __device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int q, 
   return ok;
 }
 
-__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // ---- random draws of a launch (prologue) ---------------------------------
 // All Poisson draws a launch can need are taken BEFORE the VM state is loaded
 // into registers, so the samplers never share the register budget with it:
@@ -760,7 +744,7 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
 // service lengths (rng4), speculative: only the first `used` are consumed and
 // rng4 is committed to the state recorded after draw used-1 (draws past scap
 // come from the out-of-line fallback below).
-__device__ __noinline__ uint32_t svc_fallback(uint64_t *st, const uint64_t *inc,
+__device__ __noinline__ uint32_t svc_fallback(uint64_t LDSP *st, const uint64_t LDSP *inc,
                                               const PoisConst *c) {
   Pcg r;
   r.s = U128{st[0], st[1]};
@@ -779,7 +763,7 @@ __device__ __noinline__ uint32_t svc_fallback(uint64_t *st, const uint64_t *inc,
 
 __device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, int K, int V) {
   const int lane = lane_id();
-  EnvHdr *H = L.hdr;
+  EnvHdr LDSP *H = L.hdr;
   Pcg r3 = ld_pcg(H, 2);
   int64_t need = 0;
 #pragma unroll 1
@@ -850,6 +834,10 @@ __device__ __forceinline__ void svc_commit(const Lds &L) {
 //  - a waiting VM's choice is "first visiting position whose PM fits", answered
 //    in O(P/64) from per-size fit bitmaps; the earliest VM (index order) with a
 //    fit wins; VMs before it never fit again (loads only grow);
+//  - after a FirstFit win on PM q only q's cpu threshold drops, so the cached
+//    "has a fit" bit of a later VM can change only if q fitted it before and
+//    not after (its first fit was then q or earlier; re-querying is exact
+//    either way); BestFit re-sorts, so it rebuilds and re-queries everything;
 //  - the heuristic's state (f32 view) and the env's state (f64) are disjoint,
 //    so applying each winner's env event as soon as it is decided equals
 //    deciding every action first and stepping afterwards (env.py:68-88).
@@ -857,14 +845,14 @@ template <int VPT>
 __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds &L,
                                                    const Tables &T, uint32_t (&wa)[VPT],
                                                    int policy, int32_t *act_out,
-                                                   uint8_t *valid_out) {
+                                                   uint8_t *valid_out STAMP_PARAMS) {
   const int lane = lane_id();
-  const int P = p.P, V = p.V, WAIT = p.P, NW = p.NW;
+  const int P = p.P, WAIT = p.P, NW = p.NW;
   const bool bf = policy == 1;
   uint32_t pend = 0;
 #pragma unroll
   for (int s = 0; s < VPT; s++)
-    if (s * 64 + lane < V && w_pl(wa[s]) == WAIT) pend |= 1u << s;
+    if (w_pl(wa[s]) == WAIT) pend |= 1u << s;
   uint32_t won = 0, bad = 0;
   int64_t n_place = 0;
   if (ballot(pend != 0)) {
@@ -872,40 +860,49 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
       const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
       L.fcpu[i] = fcv;
       L.fmem[i] = fmv;
-      L.tc[i] = (uint8_t)(fit_threshold(fcv, T.fcent) + 1);
-      L.tm[i] = (uint8_t)(fit_threshold(fmv, T.fcent) + 1);
+      L.tc[i] = (uint8_t)(fit_threshold(fcv) + 1);
+      L.tm[i] = (uint8_t)(fit_threshold(fmv) + 1);
     }
     wsync();
+    STAMP(16);
     bool rebuild = true;
+    uint32_t hit = 0;  // bit s: VM slot s of this lane is pending and some PM fits it
 #pragma unroll 1
     for (;;) {
       if (rebuild) {  // single site: initial build, and BF's re-sort after a win
-        if (bf) bf_sort(p, L.base);
-        build_bitmaps(p, L.base, bf);
+        if (bf) bf_sort(p, L);
+        build_bitmaps(p, L, bf);
         rebuild = false;
+        STAMP(17);
+        hit = 0;
+#pragma unroll
+        for (int s = 0; s < VPT; s++)
+          if (((pend >> s) & 1u) && bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) >= 0)
+            hit |= 1u << s;
       }
-      int ws = -1, wl = 0, wpos = 0;
+      // earliest VM (index order) with a fit
+      int ws = -1, wl = 0;
       uint32_t ww = 0;
 #pragma unroll
       for (int s = 0; s < VPT; s++) {
-        const bool pd = (pend >> s) & 1u;
-        if (ws < 0 && ballot(pd)) {
-          const int pos = pd ? bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) : -1;
-          const uint64_t m = ballot(pos >= 0);
+        if (ws < 0) {
+          const uint64_t m = ballot((hit >> s) & 1u);
           if (m) {
             ws = s;
             wl = __ffsll((unsigned long long)m) - 1;
-            wpos = __builtin_amdgcn_readlane(pos, wl);
             ww = rdlane(wa[s], wl);
           }
         }
       }
+      STAMP(18);
       if (ws < 0) break;
       // everything up to and including the winner is decided
 #pragma unroll
       for (int s = 0; s < VPT; s++)
         if (s < ws || (s == ws && lane <= wl)) pend &= ~(1u << s);
+      hit &= pend;
       const int kc = w_cc(ww), km = w_cm(ww);
+      const int wpos = bm_query(L, NW, kc, km);  // wave-uniform
       const int q = bf ? (int)L.ord[wpos] : wpos;
       const bool ok = env_place(L, T, q, kc, km);  // env.py:55-56, 58-64
       n_place += ok;
@@ -920,14 +917,16 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         if (act_out) act_out[ws * 64 + wl] = q;
       }
       // heuristic state update (f32): FF updates cpu only (firstfit.py:36)
+      const int tc_old = (int)L.tc[q] - 1;
+      wsync();
       if (lane == 0) {
         const float nc = L.fcpu[q] + T.fcent[kc];
         L.fcpu[q] = nc;
-        L.tc[q] = (uint8_t)(fit_threshold(nc, T.fcent) + 1);
+        L.tc[q] = (uint8_t)(fit_threshold(nc) + 1);
         if (bf) {
           const float nm = L.fmem[q] + T.fcent[km];
           L.fmem[q] = nm;
-          L.tm[q] = (uint8_t)(fit_threshold(nm, T.fcent) + 1);
+          L.tm[q] = (uint8_t)(fit_threshold(nm) + 1);
         }
       }
       wsync();
@@ -935,6 +934,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         rebuild = true;
       } else {  // only PM q's bit changes, for sizes above its new threshold
         const int t = (int)L.tc[q] - 1;
+        const int tmq = (int)L.tm[q] - 1;
         const int w = q >> 6;
         const uint64_t bit = 1ull << (q & 63);
         for (int k = lane; k < 101; k += 64) {
@@ -942,14 +942,24 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
           L.bc[k * NW + w] = (t >= k) ? (x | bit) : (x & ~bit);
         }
         wsync();
+        // re-query the VMs q fitted before and not after
+#pragma unroll
+        for (int s = 0; s < VPT; s++) {
+          const int c = w_cc(wa[s]);
+          const bool rq = ((hit >> s) & 1u) && c > t && c <= tc_old && w_cm(wa[s]) <= tmq;
+          if (ballot(rq)) {
+            if (rq && bm_query(L, NW, c, w_cm(wa[s])) < 0) hit &= ~(1u << s);
+          }
+        }
       }
+      STAMP(19);
     }
   }
   if (act_out || valid_out) {
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
       const int v = s * 64 + lane;
-      if (v < V) {
+      if (live(wa[s])) {
         if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(wa[s]);
         if (valid_out) valid_out[v] = (uint8_t)!((bad >> s) & 1u);
       }
@@ -967,11 +977,11 @@ __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L,
                                                uint8_t *valid_out, int64_t &n_place,
                                                int64_t &n_susp) {
   const int lane = lane_id();
-  const int P = p.P, V = p.V, WAIT = p.P;
+  const int P = p.P, WAIT = p.P;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
-    const bool in = v < V;
+    const bool in = live(wa[s]);
     const int c = w_pl(wa[s]);
     const int t = in ? act_row[v] : c;
     const bool isplace = in && c == WAIT && t >= 0 && t < P;
@@ -1035,20 +1045,15 @@ __device__ __forceinline__ double kl_reward(double tcm, double tmm, double tcv, 
 template <int VPT>
 __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, const Tables &T,
                                            uint32_t (&wa)[VPT], uint32_t (&rem)[VPT],
-                                           int kstep, bool &terminated
-#ifdef VMP_STAMPS
-                                           , uint64_t (&st_acc)[16], uint64_t &st_prev
-#endif
-) {
+                                           int kstep, bool &terminated STAMP_PARAMS) {
   const int lane = lane_id();
-  const int P = p.P, V = p.V, WAIT = p.P, NUL = p.P + 1;
-  EnvHdr *H = L.hdr;
+  const int P = p.P, WAIT = p.P, NUL = p.P + 1;
+  EnvHdr LDSP *H = L.hdr;
   // ---- _run_vms (env.py:244-268) ----
   int64_t n_term = 0;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
-    const bool in = s * 64 + lane < V;
-    const bool running = in && w_pl(wa[s]) < P;
+    const bool running = w_pl(wa[s]) < P;
     if (running && rem[s] > 0) rem[s] -= 1;
     const bool term = running && rem[s] == 0;
     uint64_t it = ballot(term);
@@ -1084,7 +1089,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
-    const bool isnull = v < V && w_pl(wa[s]) == NUL;
+    const bool isnull = w_pl(wa[s]) == NUL;
     const uint64_t nm = ballot(isnull);
     if (isnull) L.nulls[n_null + below(nm, lane)] = (uint16_t)v;
     n_null += __popcll(nm);
@@ -1121,20 +1126,23 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
   wsync();
   STAMP(3);
   // ---- stats + reward (env.py:112-156) ----
+  // target_cpu/memory_mean (env.py:116-121) feed only the kl reward and the
+  // eval-mode info; for wr/ut they are derived on demand from the stored state
+  // by k_target_means (vmp_get_stats), so the step skips the two V-long sums.
+  const bool kl = p.reward == 2;
   int n_ex = 0, n_w = 0;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
-    const bool in = s * 64 + lane < V;
     const int c = w_pl(wa[s]);
-    const bool ex = in && c <= WAIT;
+    const bool ex = c <= WAIT;
     const uint64_t em = ballot(ex);
-    if (ex) {
+    if (kl && ex) {
       const int rk = n_ex + below(em, lane);
       L.ccomp[rk] = (uint8_t)w_cc(wa[s]);
       L.mcomp[rk] = (uint8_t)w_cm(wa[s]);
     }
     n_ex += __popcll(em);
-    n_w += __popcll(ballot(in && c == WAIT));
+    n_w += __popcll(ballot(c == WAIT));
   }
   wsync();
   STAMP(11);
@@ -1144,12 +1152,12 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
   //  4,5  sum of PM cpu / memory (ut reward; kl means)
   //  6,7  PM squared-deviation sums (kl, np.var(cpu/memory))
   //  8,9  VM-size squared-deviation sums (kl, np.var(vm_cpu/vm_memory[existing]))
-  double *res = L.jobres;
+  double LDSP *res = L.jobres;
   const double *cent = T.cent;
   {  // VM-size sources: accepted sizes, existing sizes, their deviations
 #pragma unroll 1
-    for (int j = (k > 0 ? 0 : 2); j < 4; j++) {
-      const uint8_t *src = (j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp);
+    for (int j = (k > 0 ? 0 : 2); j < (kl ? 4 : 2); j++) {
+      const uint8_t LDSP *src = (j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp);
       const int n = j < 2 ? (int)k : n_ex;
       const double r = wave_pw_sum(n, [=](int i) { return cent[src[i]]; }, L.pw);
       wsync();
@@ -1161,7 +1169,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     const int jend = p.reward == 2 ? 8 : 6;
 #pragma unroll 1
     for (int j = 4; j < jend; j++) {
-      const double *src = (j & 1) ? L.mem : L.cpu;
+      const double LDSP *src = (j & 1) ? L.mem : L.cpu;
       const double mean = j < 6 ? 0.0 : res[j - 2] / (double)P;
       const bool sq = j >= 6;
       const double r = wave_pw_sum(P, [=](int i) {
@@ -1177,7 +1185,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
   if (p.reward == 2) {  // VM-size deviations (kl)
 #pragma unroll 1
     for (int j = 8; j < 10; j++) {
-      const uint8_t *src = (j & 1) ? L.mcomp : L.ccomp;
+      const uint8_t LDSP *src = (j & 1) ? L.mcomp : L.ccomp;
       const double mean = res[j - 6] / (double)n_ex;
       const double r = wave_pw_sum(n_ex, [=](int i) {
         const double d = cent[src[i]] - mean;
@@ -1190,6 +1198,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
   }
   STAMP(12);
   const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
+  if (!kl) res[2] = res[3] = 0.0;  // unused below
   double tcm = res[2] / (double)P;
   if (p.cap_target_util && tcm > 1) tcm = 1.0;
   double tmm = res[3] / (double)P;
@@ -1223,8 +1232,10 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     H->served += n_term;
     H->dropped += arrivals - k;
     H->waiting_ratio = wr;
-    H->tcm = tcm;
-    H->tmm = tmm;
+    if (kl) {
+      H->tcm = tcm;
+      H->tmm = tmm;
+    }
     if (k > 0) {
       H->total_cpu_req = H->total_cpu_req + res[0];
       H->total_mem_req = H->total_mem_req + res[1];
@@ -1242,7 +1253,7 @@ __device__ __forceinline__ void write_obs(const EnvParams &p, const Lds &L, cons
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
-    if (v < V) {
+    if (live(wa[s])) {
       obs[v] = (float)w_pl(wa[s]);
       obs[V + v] = T.fcent[w_cc(wa[s])];
       obs[2 * V + v] = T.fcent[w_cm(wa[s])];
@@ -1259,11 +1270,11 @@ template <int VPT>
 __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, const Tables &T,
                                            const uint32_t (&wa)[VPT], uint32_t *bits) {
   const int lane = lane_id();
-  const int V = p.V, P = p.P, A = p.A, W = p.W32, WAIT = p.P, NUL = p.P + 1;
+  const int P = p.P, A = p.A, W = p.W32, WAIT = p.P, NUL = p.P + 1;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
-    const bool in = v < V;
+    const bool in = live(wa[s]);
     const int c = in ? w_pl(wa[s]) : NUL;
     const double vc = T.cent[w_cc(wa[s])], vm = T.cent[w_cm(wa[s])];
     const bool waiting = in && c == WAIT;
@@ -1306,14 +1317,14 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
   const int wid = threadIdx.x >> 6;
   const int e = uni(blockIdx.x * kWavesPerBlock + wid);
   if (e >= p.N) return;
-  char *base = lds + wid * p.lds_wave_bytes;
+  char LDSP *base = (char LDSP *)lds + wid * p.lds_wave_bytes;
   const Lds L = make_lds(p, base);
   const int V = p.V, P = p.P;
   // ---- header and PM resources to LDS; the launch's random draws ----
   const double *pm = p.pm + (int64_t)e * 2 * P;
   for (int i = lane; i < 2 * P; i += 64) L.cpu[i] = pm[i];
   if (lane < 32)
-    reinterpret_cast<uint64_t *>(L.hdr)[lane] = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane];
+    reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane] = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane];
   wsync();
 #ifdef VMP_STAMPS
   const uint64_t t_loaded = __builtin_amdgcn_s_memtime();
@@ -1328,7 +1339,7 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
-    const uint64_t w = v < V ? vmw[v] : (uint64_t)(P + 1);
+    const uint64_t w = v < V ? vmw[v] : (uint64_t)kPad;
     wa[s] = (uint32_t)w;
     rem[s] = (uint32_t)(w >> 32);
   }
@@ -1348,7 +1359,7 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
     int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
     int64_t n_place = 0, n_susp = 0;
     if (o.policy >= 0)
-      n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row);
+      n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row STAMP_ARGS);
     else
       external_apply<VPT>(p, L, T, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
     STAMP(1);
@@ -1358,11 +1369,7 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
       L.hdr->suspend_action += n_susp;
     }
     wsync();
-#ifdef VMP_STAMPS
-    const double r = env_tail<VPT>(p, L, T, wa, rem, k, term, st_acc, st_prev);
-#else
-    const double r = env_tail<VPT>(p, L, T, wa, rem, k, term);
-#endif
+    const double r = env_tail<VPT>(p, L, T, wa, rem, k, term STAMP_ARGS);
     if (o.reward && lane == 0) o.reward[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
@@ -1372,7 +1379,7 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
     uint32_t wt[VPT];
 #pragma unroll
     for (int s = 0; s < VPT; s++) wt[s] = wa[s];
-    heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr);
+    heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr STAMP_ARGS);
   }
   STAMP(0);
   if (o.obs) write_obs<VPT>(p, L, T, wa, o.obs + (int64_t)e * p.D);
@@ -1385,12 +1392,12 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
       const int v = s * 64 + lane;
-      if (v < V) vmo[v] = (uint64_t)wa[s] | ((uint64_t)rem[s] << 32);
+      if (live(wa[s])) vmo[v] = (uint64_t)wa[s] | ((uint64_t)rem[s] << 32);
     }
     double *pmo = p.pm + (int64_t)e * 2 * P;
     for (int i = lane; i < 2 * P; i += 64) pmo[i] = L.cpu[i];
     if (lane < 32)
-      reinterpret_cast<uint64_t *>(p.hdr + e)[lane] = reinterpret_cast<uint64_t *>(L.hdr)[lane];
+      reinterpret_cast<uint64_t *>(p.hdr + e)[lane] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane];
   }
   STAMP(6);
 #ifdef VMP_STAMPS
@@ -1481,6 +1488,50 @@ __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double
       r += used;
     }
     rank[i] = r;
+  }
+}
+
+// target_cpu_mean / target_memory_mean (env.py:116-121) from the stored state,
+// one wave per env. Both are pure functions of the post-step state (existing =
+// placement <= WAIT, their sizes in index order), so deriving them here gives
+// the values step() would have left, through the same pairwise order; the step
+// kernel itself computes them only for the kl reward. vmp_get_stats runs this
+// before k_counters.
+__global__ __launch_bounds__(256) void k_target_means(EnvParams p) {
+  __shared__ uint8_t comp[kWavesPerBlock][2][kMaxVPT * 64];
+  __shared__ double cent[128];
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) cent[i] = (double)i / 100.0;
+  __syncthreads();
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const int e = uni(blockIdx.x * kWavesPerBlock + wid);
+  if (e >= p.N) return;
+  const int V = p.V, P = p.P;
+  const uint64_t *row = p.vmw + (int64_t)e * V;
+  uint8_t *cc = comp[wid][0], *cm = comp[wid][1];
+  int n_ex = 0;
+  for (int b = 0; b < V; b += 64) {
+    const int v = b + lane;
+    const uint64_t w = v < V ? row[v] : (uint64_t)(P + 1);
+    const bool ex = v < V && (int)(w & 0xFFFFu) <= P;
+    const uint64_t m = ballot(ex);
+    if (ex) {
+      const int rk = n_ex + below(m, lane);
+      cc[rk] = (uint8_t)((w >> 16) & 0xFFu);
+      cm[rk] = (uint8_t)((w >> 24) & 0xFFu);
+    }
+    n_ex += __popcll(m);
+  }
+  wsync();
+  const PwLds none{};  // n <= 1024: the register plan, no LDS plan needed
+  const double *ct = cent;
+  const double sc = wave_pw_sum(n_ex, [=](int i) { return ct[cc[i]]; }, none);
+  const double sm = wave_pw_sum(n_ex, [=](int i) { return ct[cm[i]]; }, none);
+  if (lane == 0) {
+    double tcm = sc / (double)P, tmm = sm / (double)P;
+    if (p.cap_target_util && tcm > 1) tcm = 1.0;
+    if (p.cap_target_util && tmm > 1) tmm = 1.0;
+    p.hdr[e].tcm = tcm;
+    p.hdr[e].tmm = tmm;
   }
 }
 
