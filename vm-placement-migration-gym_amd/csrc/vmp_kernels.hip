@@ -874,11 +874,27 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         build_bitmaps(p, L, bf);
         rebuild = false;
         STAMP(17);
+        // which pending VMs have any fit: branch-free row ANDs for P <= 128
+        // (every slot's rows are valid, pad slots read row 0), so the LDS
+        // reads of all slots are in flight together
         hit = 0;
+        if (NW <= 2) {
+          const int nw = NW;
 #pragma unroll
-        for (int s = 0; s < VPT; s++)
-          if (((pend >> s) & 1u) && bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) >= 0)
-            hit |= 1u << s;
+          for (int s = 0; s < VPT; s++) {
+            const uint64_t LDSP *rc = L.bc + w_cc(wa[s]) * nw;
+            const uint64_t LDSP *rm = L.bm + w_cm(wa[s]) * nw;
+            uint64_t a = rc[0] & rm[0];
+            if (nw == 2) a |= rc[1] & rm[1];
+            hit |= (uint32_t)(a != 0) << s;
+          }
+          hit &= pend;
+        } else {
+#pragma unroll
+          for (int s = 0; s < VPT; s++)
+            if (((pend >> s) & 1u) && bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) >= 0)
+              hit |= 1u << s;
+        }
       }
       // earliest VM (index order) with a fit
       int ws = -1, wl = 0;
@@ -1320,11 +1336,34 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
   char LDSP *base = (char LDSP *)lds + wid * p.lds_wave_bytes;
   const Lds L = make_lds(p, base);
   const int V = p.V, P = p.P;
-  // ---- header and PM resources to LDS; the launch's random draws ----
+  // ---- every global load of the env's state is issued up front: header and
+  // PM resources (needed first, to LDS), then the VM words (to registers),
+  // whose latency the random draws below overlap ----
+  // (indices are clamped instead of branched on, so no load is conditional and
+  // the waits below can count: a skipped load would force vmcnt(0))
+  const uint64_t hv = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane & 31];
   const double *pm = p.pm + (int64_t)e * 2 * P;
-  for (int i = lane; i < 2 * P; i += 64) L.cpu[i] = pm[i];
-  if (lane < 32)
-    reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane] = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane];
+  const int n_pm = 2 * P;
+  double pv[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) pv[j] = pm[min(j * 64 + lane, n_pm - 1)];
+  __asm__ volatile("" ::: "memory");  // keep the issue order: header/PM first
+  const uint64_t *vmw = p.vmw + (int64_t)e * V;
+  uint32_t wa[VPT], rem[VPT];
+#pragma unroll
+  for (int s = 0; s < VPT; s++) {
+    const int v = s * 64 + lane;
+    const uint64_t x = vmw[min(v, V - 1)];
+    const uint64_t w = v < V ? x : (uint64_t)kPad;
+    wa[s] = (uint32_t)w;
+    rem[s] = (uint32_t)(w >> 32);
+  }
+  __asm__ volatile("" ::: "memory");  // ... and the VM words before any wait
+  if (lane < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane] = hv;
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if (j * 64 + lane < n_pm) L.cpu[j * 64 + lane] = pv[j];
+  for (int i = 256 + lane; i < n_pm; i += 64) L.cpu[i] = pm[i];  // P > 128
   wsync();
 #ifdef VMP_STAMPS
   const uint64_t t_loaded = __builtin_amdgcn_s_memtime();
@@ -1333,16 +1372,6 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
 #ifdef VMP_STAMPS
   const uint64_t t_drawn = __builtin_amdgcn_s_memtime();
 #endif
-  // ---- VM words to registers ----
-  const uint64_t *vmw = p.vmw + (int64_t)e * V;
-  uint32_t wa[VPT], rem[VPT];
-#pragma unroll
-  for (int s = 0; s < VPT; s++) {
-    const int v = s * 64 + lane;
-    const uint64_t w = v < V ? vmw[v] : (uint64_t)kPad;
-    wa[s] = (uint32_t)w;
-    rem[s] = (uint32_t)(w >> 32);
-  }
   STAMP_DECL
 #ifdef VMP_STAMPS
   st_acc[13] = t_loaded - t_start;
