@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 1
+#define VMP_ABI_VERSION 2
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -46,6 +46,11 @@ extern "C" {
 #define VMP_SEQ_UNIFORM 0
 #define VMP_SEQ_LOWUNIFORM 1
 #define VMP_SEQ_HIGHUNIFORM 2
+/* actor-head modes (vmp_policy_head) */
+#define VMP_HEAD_SAMPLE 0 /* Network.get_action(obs, action=None, mask) (ppo.py:115-126) */
+#define VMP_HEAD_GIVEN 1  /* Network.get_action(obs, action, mask): log_prob/entropy only */
+#define VMP_HEAD_ARGMAX 2 /* Network.get_det_action (ppo.py:128-131): unmasked argmax */
+#define VMP_HEAD_MAX_A 1024 /* action_dim limit of the register-resident row */
 /* heuristic policies (src/agents/firstfit.py:21-38, bestfit.py:21-40) */
 #define VMP_POLICY_FIRSTFIT 0
 #define VMP_POLICY_BESTFIT 1
@@ -160,14 +165,36 @@ int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const 
             const float *next_value, float gamma, float lam, float *adv, float *ret,
             void *hip_stream);
 
-/* Masked multi-categorical sampling (ppo.py:115-126): logits f32[B][V*A],
- * mask bits u32[B][V][W] (nullable = unmasked; masked logits are set to -1e7
- * as ppo.py:119 does), uniforms for Gumbel-max from (seed, offset).
- * Outputs per (sample, VM) row: action int32[B][V], logprob f32[B][V],
- * entropy f32[B][V] (the caller sums over V as ppo.py:124-125 does). */
-int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
-                      const uint32_t *mask_bits, uint64_t seed, uint64_t offset,
-                      int32_t *action, float *logprob, float *entropy, void *hip_stream);
+/* Network.get_action head (ppo.py:115-126) on the actor's logits f32[B][V*A]
+ * (row-major, as nn.Linear writes them): rows flagged in mask_bits u32[B][V][W]
+ * (W = ceil(A/32), nullable = get_action(..., invalid_mask=None)) are set to
+ * -1e7 as ppo.py:119 does, then per (b, v) a Categorical over A.
+ *  - VMP_HEAD_SAMPLE: action[b][v] drawn (inverse CDF, counter-based uniforms
+ *    from (seed, offset + b*V + v)); VMP_HEAD_GIVEN: action read.
+ *    logprob[b] = sum_v log p(action), entropy[b] = sum_v H (ppo.py:123-126),
+ *    both nullable.
+ *  - VMP_HEAD_ARGMAX: get_det_action (ppo.py:128-131), argmax of the unmasked
+ *    row, first index on ties; logprob/entropy untouched.
+ *  - wait_ratio >= 0 applies PPOAgent.act's WAIT coin flips first (ppo.py:154-156):
+ *    a row with > 1 invalid entries whose column wait_index (= P) is valid
+ *    gets it forbidden when a uniform draw exceeds wait_ratio
+ *    (migration_ratio). wait_ratio < 0: no flips (PPOAgent.learn, ppo.py:197).
+ * Replaces the torch Categorical / multinomial calls of ppo.py:117-126.
+ * All pointers are device pointers; A <= VMP_HEAD_MAX_A. */
+int vmp_policy_head(int32_t B, int32_t V, int32_t A, int32_t mode, const float *logits,
+                    const uint32_t *mask_bits, float wait_ratio, int32_t wait_index,
+                    uint64_t seed, uint64_t offset, int32_t *action, float *logprob,
+                    float *entropy, void *hip_stream);
+
+/* Backward of vmp_policy_head (VMP_HEAD_SAMPLE/GIVEN, no coin flips) for the
+ * PPO loss (ppo.py:258-277): given dL/dlogprob[B] and dL/dentropy[B]
+ * (nullable = 0), writes dL/dlogits f32[B][V*A]; masked entries get 0 (the
+ * in-place mask assignment of ppo.py:119 passes no gradient). dlogits may
+ * alias logits (the rows are read before they are written). */
+int vmp_policy_head_backward(int32_t B, int32_t V, int32_t A, const float *logits,
+                             const uint32_t *mask_bits, const int32_t *action,
+                             const float *g_logprob, const float *g_entropy, float *dlogits,
+                             void *hip_stream);
 
 /* Diagnostics: per-env shader-clock cycles per kernel phase, accumulated since
  * the previous call, device u64[n_env][24] (see tools/stamps.py for the phase names).

@@ -1,0 +1,209 @@
+"""PPO host logic on CPU (no GPU): the torch reference head against the
+reference Network's recorded outputs, PPOAgent.update against one reference
+update() (tests/golden/ppo_update.npz, tools/gen_golden.py), the batched /
+chunked / data-parallel update against the single-process one, weights I/O and
+mask packing. The HIP ops are injected out (head=torch_head, gae=torch_gae);
+their own parity is tests/test_gpu_ppo.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from tests.torch_ref import StubEnv, torch_gae, torch_head, unpack_bits
+from vmp.config import Config
+from vmp.head import pack_mask
+from vmp.ppo import Network, PPOAgent, PPOConfig, strip_compiled_prefix
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+CFG10 = dict(arrival_rate=0.182, service_length=100, pms=10, vms=30, training_steps=10000,
+             eval_steps=200, seed=1, reward_function="wr", allow_null_action=True)
+
+
+def _golden(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def _agent(hidden=64, n_envs=1, **kw):
+    return PPOAgent(StubEnv(Config(**CFG10), n_envs=n_envs),
+                    PPOConfig(hidden_size=hidden, episodes=1, **kw), head=torch_head,
+                    gae=torch_gae)
+
+
+def test_pack_mask_roundtrip():
+    g = torch.Generator().manual_seed(0)
+    for V, A in ((30, 12), (7, 32), (5, 33), (3, 102), (2, 1002)):
+        m = torch.rand((4, V, A), generator=g) < 0.4
+        bits = pack_mask(m, V, A)
+        assert bits.dtype == torch.int32 and bits.shape == (4, V, (A + 31) // 32)
+        assert torch.equal(unpack_bits(bits, A), m)
+        assert torch.equal(pack_mask(bits, V, A), bits)  # int32 words pass through
+
+
+def test_torch_head_matches_reference_network_outputs():
+    """The torch reference op reproduces the reference Network (weights-10/ppo-wr.pt)
+    logprob/entropy with and without the mask."""
+    w, f = _golden("ppo10_wr_weights.npz"), _golden("ppo10_fwd.npz")
+    net = Network(110, np.full(30, 12), 512, head=torch_head)
+    net.load_state_dict({k: torch.tensor(w[k]) for k in w.files})
+    obs = torch.tensor(f["obs"])
+    with torch.no_grad():
+        logits = net.actor(obs)
+        value = net.get_value(obs)
+        assert torch.allclose(logits, torch.tensor(f["logits"]), rtol=1e-5, atol=1e-5)
+        assert torch.allclose(value, torch.tensor(f["value"]), rtol=1e-5, atol=1e-5)
+        act = torch.tensor(f["action"])
+        _, lp, ent = net.get_action(obs, action=act, invalid_mask=torch.tensor(f["mask"]))
+        assert np.allclose(lp.numpy(), f["logprob"], rtol=1e-5, atol=1e-5)
+        assert np.allclose(ent.numpy(), f["entropy"], rtol=1e-5, atol=1e-5)
+        _, lp, ent = net.get_action(obs, action=act)
+        assert np.allclose(lp.numpy(), f["logprob_nomask"], rtol=1e-5, atol=1e-5)
+        assert np.allclose(ent.numpy(), f["entropy_nomask"], rtol=1e-5, atol=1e-5)
+        det = logits.reshape(-1, 30, 12).argmax(-1)
+        assert np.array_equal(det.numpy(), f["det"])
+
+
+def _batch(d):
+    return [torch.tensor(d[k]) for k in ("b_mask", "b_action", "b_obs", "b_next_obs",
+                                         "b_logprob", "b_reward", "b_done")]
+
+
+def test_update_matches_reference_update():
+    """PPOAgent.update (ppo.py:229-295) on the recorded batch: parameters after
+    the 16 AdamW steps equal the reference's within 1e-6 absolute (the update
+    moves them by ~8e-4), incl. the [mb,1]-[mb] value-loss broadcast."""
+    d = _golden("ppo_update.npz")
+    ag = _agent()
+    ag.model.load_state_dict({k[3:]: torch.tensor(d[k]) for k in d.files if k.startswith("p0_")})
+    st = ag.update(*_batch(d))
+    assert st["minibatches"] == 16 and st["kl_breaks"] == 0
+    for k, v in ag.model.state_dict().items():
+        p0, p1 = d["p0_" + k], d["p1_" + k]
+        assert np.abs(p1 - p0).max() > 1e-4, k
+        np.testing.assert_allclose(v.numpy(), p1, rtol=0, atol=1e-6, err_msg=k)
+
+
+def test_elementwise_value_loss_differs():
+    """value_loss_broadcast=False is a real change of the loss (not the reference)."""
+    d = _golden("ppo_update.npz")
+    ag = _agent(value_loss_broadcast=False)
+    ag.model.load_state_dict({k[3:]: torch.tensor(d[k]) for k in d.files if k.startswith("p0_")})
+    ag.update(*_batch(d))
+    v = ag.model.state_dict()["critic.4.weight"].numpy()
+    assert np.abs(v - d["p1_critic.4.weight"]).max() > 1e-5
+
+
+def _synthetic_rollout(T, N, V=30, A=12, D=110, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    obs = torch.rand((T, N, D), generator=g)
+    mask = torch.rand((T, N, V, A), generator=g) < 0.5
+    mask[..., 10] = False  # WAIT always valid -> no all-masked rows
+    act = torch.zeros((T, N, V), dtype=torch.int32)
+    for idx in np.ndindex(T, N, V):
+        ok = torch.nonzero(~mask[idx]).flatten()
+        act[idx] = ok[torch.randint(len(ok), (1,), generator=g)]
+    bits = pack_mask(mask.reshape(T * N, V, A), V, A).reshape(T, N, V, -1)
+    lp = -torch.rand((T, N), generator=g) * 30
+    rew = -torch.rand((T, N), generator=g)
+    done = torch.zeros((T, N))
+    done[T // 2, :] = 1
+    return obs, bits, act, lp, rew, done
+
+
+def _trainer_update(ag, roll, n_slice=None, group=None):
+    from vmp.ppo import PPOTrainer
+    obs, bits, act, lp, rew, done = roll
+    if n_slice is not None:
+        obs, bits, act, lp, rew, done = (x[:, n_slice].contiguous() for x in roll)
+    tr = PPOTrainer(ag, group=group, allocate=False)
+    T, N = rew.shape
+    with torch.no_grad():
+        values = ag.model.get_value(obs.reshape(T * N, -1)).reshape(T, N)
+        nv = torch.zeros_like(values)
+        nv[:-1] = values[1:]
+    return tr.update_from(obs, bits, act, lp, rew, done, values, nv)
+
+
+def test_chunked_update_equals_unchunked():
+    torch.manual_seed(3)
+    roll = _synthetic_rollout(T=20, N=6)
+    sd = None
+    out = []
+    for cb in (1 << 40, 5 * 30 * 12 * 4 * 2):  # one chunk / 2-env chunks
+        ag = _agent(n_envs=6, batch_size=20, minibatch_size=5, chunk_bytes=cb)
+        if sd is None:
+            sd = {k: v.clone() for k, v in ag.model.state_dict().items()}
+        ag.model.load_state_dict(sd)
+        _trainer_update(ag, roll)
+        out.append(ag.model.state_dict())
+    for k in out[0]:
+        torch.testing.assert_close(out[0][k], out[1][k], rtol=0, atol=2e-7)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, sd, roll, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N = roll[0].shape[1] // world
+        ag = _agent(n_envs=N, batch_size=20, minibatch_size=5)
+        ag.model.load_state_dict(sd)
+        st = _trainer_update(ag, roll, n_slice=slice(rank * N, (rank + 1) * N))
+        # numpy by value: torch tensors would travel as fds of a process about to exit
+        q.put((rank, {k: v.numpy().copy() for k, v in ag.model.state_dict().items()},
+               st["kl_breaks"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_update_equals_single_process():
+    """envs sharded over 2 gloo ranks, global advantage
+    normalisation + KL test + one flat-gradient all-reduce per step -> the same
+    parameters as one process updating on all envs."""
+    torch.manual_seed(5)
+    roll = _synthetic_rollout(T=20, N=4, seed=1)
+    ag = _agent(n_envs=4, batch_size=20, minibatch_size=5)
+    sd = {k: v.clone() for k, v in ag.model.state_dict().items()}
+    _trainer_update(ag, roll)
+    ref = ag.model.state_dict()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, sd, roll, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (s, kb)) for r, s, kb in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        for k in ref:
+            np.testing.assert_allclose(res[r][0][k], ref[k].numpy(), rtol=0, atol=2e-6)
+    for k in ref:  # ranks stay bit-identical
+        assert np.array_equal(res[0][0][k], res[1][0][k])
+
+
+def test_weights_io_compiled_prefix(tmp_path):
+    """save_model writes the reference's torch.compile keys; load_model reads both."""
+    w = _golden("ppo10_wr_weights.npz")
+    ag = _agent(hidden=512)
+    ag.model.load_state_dict({k: torch.tensor(w[k]) for k in w.files})
+    p = str(tmp_path / "w" / "ppo.pt")
+    ag.save_model(p)
+    sd = torch.load(p, weights_only=True)
+    assert all(k.startswith("_orig_mod.") for k in sd)
+    assert sorted(strip_compiled_prefix(sd)) == sorted(w.files)
+    ag2 = _agent(hidden=512)
+    ag2.load_model(p)
+    for k, v in ag2.model.state_dict().items():
+        assert np.array_equal(v.numpy(), w[k])

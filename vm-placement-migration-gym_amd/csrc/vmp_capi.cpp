@@ -23,11 +23,6 @@ __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double
 __global__ void k_counters(EnvParams p, int64_t *ctr, double *st);
 __global__ void k_target_means(EnvParams p);
 __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, uint8_t *mask);
-__global__ void k_gae(int T, int N, const float *r, const float *d, const float *v,
-                      const float *nv, float gamma, float lam, float *adv, float *ret);
-__global__ void k_masked_sample(int B, int V, int A, int W, const float *logits,
-                                const uint32_t *bits, uint64_t seed, uint64_t offset,
-                                int32_t *action, float *lp_row, float *ent_row);
 }  // namespace vmp
 
 using namespace vmp;
@@ -74,6 +69,11 @@ double loggam_host(double x) {
 }
 
 }  // namespace
+
+namespace vmp {
+// error reporting for the policy kernels (vmp_policy.hip) through vmp_last_error()
+int policy_fail(int code, const char *msg) { return fail(code, msg); }
+}  // namespace vmp
 
 struct vmp_handle {
   vmp_config cfg;
@@ -485,33 +485,6 @@ int vmp_get_rank(vmp_handle *h, int64_t *rank) {
   if (!h || !rank) return fail(VMP_EINVAL, "null argument");
   hipLaunchKernelGGL(k_export, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,
                      nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, rank);
-  HIP_TRY(hipGetLastError());
-  return VMP_OK;
-}
-
-int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const float *value,
-            const float *next_value, float gamma, float lam, float *adv, float *ret,
-            void *stream) {
-  if (T < 0 || N < 0 || !reward || !done || !value || !next_value || !adv || !ret)
-    return fail(VMP_EINVAL, "bad gae arguments");
-  if (T == 0 || N == 0) return VMP_OK;
-  hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, T, N,
-                     reward, done, value, next_value, gamma, lam, adv, ret);
-  HIP_TRY(hipGetLastError());
-  return VMP_OK;
-}
-
-int vmp_masked_sample(int32_t B, int32_t V, int32_t A, const float *logits,
-                      const uint32_t *mask_bits, uint64_t seed, uint64_t offset, int32_t *action,
-                      float *logprob_row, float *entropy_row, void *stream) {
-  if (B < 0 || V < 1 || A < 1 || !logits || !action || !logprob_row || !entropy_row)
-    return fail(VMP_EINVAL, "bad sample arguments");
-  int64_t rows = (int64_t)B * V;
-  if (rows == 0) return VMP_OK;
-  int W = (A + 31) / 32;
-  hipLaunchKernelGGL(k_masked_sample, dim3((unsigned)((rows + kWavesPerBlock - 1) / kWavesPerBlock)),
-                     dim3(64 * kWavesPerBlock), 0, (hipStream_t)stream, B, V, A, W, logits,
-                     mask_bits, seed, offset, action, logprob_row, entropy_row);
   HIP_TRY(hipGetLastError());
   return VMP_OK;
 }

@@ -1595,92 +1595,4 @@ __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, ui
   mask[i] = (bits[r * W + (a >> 5)] >> (a & 31)) & 1u;
 }
 
-// ----------------------------------------------------------------- GAE ---
-// PPOAgent.update advantage scan (ppo.py:232-243), one lane per env column.
-__global__ void k_gae(int T, int N, const float *r, const float *d, const float *v,
-                      const float *nv, float gamma, float lam, float *adv, float *ret) {
-  int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float g = 0.f;
-  for (int t = T - 1; t >= 0; t--) {
-    int64_t i = (int64_t)t * N + n;
-    float nd = 1.f - d[i];
-    float delta = r[i] + nd * gamma * nv[i] - v[i];
-    g = delta + nd * gamma * lam * g;
-    adv[i] = g;
-    ret[i] = g + v[i];
-  }
-}
-
-// ------------------------------------------------ masked categorical -----
-// One wave per (sample, VM) row of A logits: mask to -1e7 (ppo.py:119),
-// log-softmax, Gumbel-max sample, log_prob and entropy; per-sample sums by
-// atomics on the row's sample. Philox-free counter hash for the uniforms.
-__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
-__global__ __launch_bounds__(256) void k_masked_sample(int B, int V, int A, int W,
-                                                       const float *logits,
-                                                       const uint32_t *bits, uint64_t seed,
-                                                       uint64_t offset, int32_t *action,
-                                                       float *lp_row, float *ent_row) {
-  const int lane = lane_id();
-  const int64_t row = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (row >= (int64_t)B * V) return;
-  const float *lg = logits + row * A;
-  const uint32_t *mb = bits ? bits + row * W : nullptr;
-  float mx = -INFINITY;
-  for (int a = lane; a < A; a += 64) {
-    float x = lg[a];
-    if (mb && ((mb[a >> 5] >> (a & 31)) & 1u)) x = -1e7f;
-    mx = fmaxf(mx, x);
-  }
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  float se = 0.f;
-  float best = -INFINITY;
-  int bi = 0;
-  for (int a = lane; a < A; a += 64) {
-    float x = lg[a];
-    if (mb && ((mb[a >> 5] >> (a & 31)) & 1u)) x = -1e7f;
-    se += expf(x - mx);
-    uint64_t h = splitmix(seed ^ splitmix(offset + (uint64_t)row * (uint64_t)A + a));
-    float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
-    float g = x - logf(-logf(u));
-    if (g > best) {
-      best = g;
-      bi = a;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    se += __shfl_xor(se, o);
-    float ob = __shfl_xor(best, o);
-    int oi = __shfl_xor(bi, o);
-    if (ob > best || (ob == best && oi < bi)) {
-      best = ob;
-      bi = oi;
-    }
-  }
-  float lse = mx + logf(se);
-  float ent = 0.f;
-  for (int a = lane; a < A; a += 64) {
-    float x = lg[a];
-    if (mb && ((mb[a >> 5] >> (a & 31)) & 1u)) x = -1e7f;
-    float lp = x - lse;
-    ent -= expf(lp) * lp;
-  }
-  for (int o = 32; o > 0; o >>= 1) ent += __shfl_xor(ent, o);
-  if (lane == 0) {
-    float xs = lg[bi];
-    if (mb && ((mb[bi >> 5] >> (bi & 31)) & 1u)) xs = -1e7f;
-    action[row] = bi;
-    lp_row[row] = xs - lse;
-    ent_row[row] = ent;
-  }
-}
-
-
 }  // namespace vmp

@@ -1,0 +1,405 @@
+// vmp_policy.hip — gfx950 kernels for the PPO side of the path
+// (src/agents/ppo.py): the masked multi-categorical actor head of
+// Network.get_action / get_det_action (ppo.py:115-131) forward and backward,
+// the PPOAgent.act WAIT coin flips (ppo.py:154-156), and the GAE reverse scan
+// of PPOAgent.update (ppo.py:232-243).
+//
+// Head layout: logits f32 [B][V][A] (the actor's last Linear output, row-major
+// [B, V*A] exactly as ppo.py:116 produces it), invalid-action bits u32
+// [B][V][W] (W = ceil(A/32), bit set = invalid, the layout vmp_mask writes).
+// One workgroup per sample b; its lanes form groups of G lanes, one group per
+// (b, v) row at a time; lane g of a group holds elements j = g + G*e (e < E) of
+// the row in registers, so each wave load reads G consecutive floats per row
+// and 64/G adjacent rows (coalesced, every byte read once). Row reductions are
+// xor shuffles inside the group; the per-sample sums over V (ppo.py:124-125)
+// are a fixed-order block reduction (deterministic, no atomics).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/vmp.h"
+
+namespace vmp {
+
+constexpr float kMaskedLogit = -1e7f;  // ppo.py:119 `logits[invalid_mask] = -1e7`
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+// Counter-based uniform in [0, 1) with 24 random bits: stream (seed, ctr).
+__device__ __forceinline__ float uniform_at(uint64_t seed, uint64_t ctr) {
+  uint64_t h = mix64(seed ^ mix64(ctr));
+  return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+
+template <int G>
+__device__ __forceinline__ float gsum(float x) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+template <int G>
+__device__ __forceinline__ float gmax(float x) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+template <int G>
+__device__ __forceinline__ int gmaxi(int x) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
+  return x;
+}
+
+struct HeadArgs {
+  int B, V, A, W, mode, wait_index;
+  float wait_ratio;
+  uint64_t seed, offset;
+  const float *logits;
+  const uint32_t *bits;
+  int32_t *action;       // in (GIVEN) or out (SAMPLE / ARGMAX), [B][V]
+  float *logprob;        // [B] (nullable)
+  float *entropy;        // [B] (nullable)
+  const float *g_logprob, *g_entropy;  // backward: dL/dlogprob[B], dL/dentropy[B]
+  float *dlogits;        // backward output [B][V][A] (may alias logits)
+};
+
+// Loads one row into registers with the mask applied and, for SAMPLE/GIVEN,
+// the WAIT coin flip of PPOAgent.act (ppo.py:154-156):
+//   count_nonzero(invalid[row]) > 1 and not invalid[row, P] and rand() > ratio
+//   -> invalid[row, P] = True.
+template <int G, int E>
+__device__ __forceinline__ void load_row(const HeadArgs &a, int64_t row, int g, float (&x)[E],
+                                         float (&raw)[E], bool flip_wait) {
+  const float *lg = a.logits + row * a.A;
+  const uint32_t *mb = a.bits ? a.bits + row * a.W : nullptr;
+  bool forbid_wait = false;
+  if (mb && flip_wait) {
+    int cnt = 0;
+    for (int w = 0; w < a.W; w++) {
+      uint32_t word = mb[w];
+      int lo = w * 32;
+      if (a.A - lo < 32) word &= (1u << (a.A - lo)) - 1u;
+      cnt += __popc(word);
+    }
+    int P = a.wait_index;
+    bool wait_bad = (mb[P >> 5] >> (P & 31)) & 1u;
+    if (cnt > 1 && !wait_bad)
+      forbid_wait = uniform_at(a.seed ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio;
+  }
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    int j = g + G * e;
+    float v = -INFINITY, r = -INFINITY;
+    if (j < a.A) {
+      r = v = lg[j];
+      if (mb && (((mb[j >> 5] >> (j & 31)) & 1u) || (forbid_wait && j == a.wait_index)))
+        v = kMaskedLogit;
+    }
+    x[e] = v;
+    raw[e] = r;
+  }
+}
+
+// Softmax statistics of a register-resident row: p[e] = exp(x - max),
+// S = sum p, lse = max + log S, H = -sum (p/S)(x - lse) (Categorical.entropy).
+template <int G, int E>
+__device__ __forceinline__ void row_stats(const float (&x)[E], int g, int A, float (&p)[E],
+                                          float &S, float &lse, float &H) {
+  float mx = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < E; e++)
+    if (g + G * e < A) mx = fmaxf(mx, x[e]);
+  mx = gmax<G>(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    p[e] = (g + G * e < A) ? expf(x[e] - mx) : 0.f;
+    s += p[e];
+  }
+  S = gsum<G>(s);
+  lse = mx + logf(S);
+  float inv = 1.0f / S, h = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; e++)
+    if (p[e] > 0.f) h += (p[e] * inv) * (x[e] - lse);
+  H = -gsum<G>(h);
+}
+
+// Inverse-CDF draw over the row in lane-major order (lane g's E elements, then
+// lane g+1's ...): any fixed order of the categories samples the same law.
+template <int G, int E>
+__device__ __forceinline__ int sample_row(const float (&p)[E], int g, int A, float u) {
+  float t = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; e++) t += p[e];
+  float incl = t;
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    float y = __shfl_up(incl, o, G);
+    if (g >= o) incl += y;
+  }
+  float excl = __shfl_up(incl, 1, G);
+  if (g == 0) excl = 0.f;
+  float total = __shfl(incl, G - 1, G);
+  float target = u * total;
+  int pick = -1, last = -1;
+  float c = excl;
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    if (p[e] > 0.f) {
+      c += p[e];
+      last = g * E + e;
+      if (pick < 0 && target >= excl && target < incl && target < c) pick = g + G * e;
+    }
+  }
+  if (pick < 0 && t > 0.f && target >= excl && target < incl) pick = g + G * ((last - g * E));
+  int any = gmaxi<G>(pick);
+  if (any >= 0) return any;
+  // target fell past the rounded total: take the last positive category
+  int lk = gmaxi<G>(last);
+  int lg = lk / E, le = lk - lg * E;
+  return lg + G * le;
+}
+
+// Block-wide fixed-order sum of one value per group leader; result in thread 0.
+template <int G>
+__device__ __forceinline__ float block_sum_groups(float v, float *lds) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o >= G; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  float s = 0.f;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < (int)(blockDim.x >> 6); w++) s += lds[w];
+  return s;
+}
+
+// Forward: mode VMP_HEAD_SAMPLE draws action[b][v]; VMP_HEAD_GIVEN reads it;
+// both write logprob[b] = sum_v log_softmax(masked)[a] and entropy[b] =
+// sum_v H_v (ppo.py:117-126). VMP_HEAD_ARGMAX is get_det_action (ppo.py:128-131):
+// argmax of the UNMASKED row, first index on ties (torch.argmax).
+template <int G, int E>
+__global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
+  __shared__ float lds[2][4];
+  const int b = blockIdx.x;
+  const int g = threadIdx.x & (G - 1);
+  const int grp = threadIdx.x / G, ngrp = blockDim.x / G;
+  const bool sample = a.mode == VMP_HEAD_SAMPLE, argmax = a.mode == VMP_HEAD_ARGMAX;
+  const bool flip = a.wait_ratio >= 0.f && !argmax;
+  float lp_acc = 0.f, ent_acc = 0.f;
+  for (int v = grp; v < a.V; v += ngrp) {
+    const int64_t row = (int64_t)b * a.V + v;
+    float x[E], raw[E], p[E];
+    load_row<G, E>(a, row, g, x, raw, flip);
+    if (argmax) {
+      float best = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int e = 0; e < E; e++) {  // strict > keeps the first index of a tie
+        int j = g + G * e;
+        if (j < a.A && raw[e] == raw[e] && (raw[e] > best || bi == 0x7fffffff)) {
+          best = raw[e];
+          bi = j;
+        }
+      }
+#pragma unroll
+      for (int o = G / 2; o > 0; o >>= 1) {
+        float ob = __shfl_xor(best, o);
+        int oi = __shfl_xor(bi, o);
+        if (ob > best || (ob == best && oi < bi)) {
+          best = ob;
+          bi = oi;
+        }
+      }
+      if (g == 0) a.action[row] = bi == 0x7fffffff ? 0 : bi;
+      continue;
+    }
+    float S, lse, H;
+    row_stats<G, E>(x, g, a.A, p, S, lse, H);
+    int act;
+    if (sample) {
+      act = sample_row<G, E>(p, g, a.A, uniform_at(a.seed, a.offset + (uint64_t)row));
+      if (g == 0) a.action[row] = act;
+    } else {
+      act = a.action[row];
+    }
+    float xa = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; e++)
+      if (g + G * e == act) xa = x[e];
+    xa = gsum<G>(xa);
+    float lp = (act >= 0 && act < a.A) ? xa - lse : NAN;
+    lp_acc += lp;
+    ent_acc += H;
+  }
+  if (argmax) return;
+  // one value per group (all lanes of a group agree); count each group once
+  float lp_v = (g == 0) ? lp_acc : 0.f, en_v = (g == 0) ? ent_acc : 0.f;
+  float lp_s = block_sum_groups<G>(lp_v, lds[0]);
+  float en_s = block_sum_groups<G>(en_v, lds[1]);
+  if (threadIdx.x == 0) {
+    if (a.logprob) a.logprob[b] = lp_s;
+    if (a.entropy) a.entropy[b] = en_s;
+  }
+}
+
+// Backward of (logprob, entropy) w.r.t. the pre-mask logits:
+//   d/dz_j = g_lp (1[j=a] - q_j) - g_ent q_j (log q_j + H),  q = softmax(masked z),
+// and 0 at masked entries (the in-place `logits[mask] = -1e7` of ppo.py:119
+// passes no gradient there). Recomputes the row statistics from the logits.
+template <int G, int E>
+__global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
+  const int b = blockIdx.x;
+  const int g = threadIdx.x & (G - 1);
+  const int grp = threadIdx.x / G, ngrp = blockDim.x / G;
+  const float glp = a.g_logprob ? a.g_logprob[b] : 0.f;
+  const float gen = a.g_entropy ? a.g_entropy[b] : 0.f;
+  for (int v = grp; v < a.V; v += ngrp) {
+    const int64_t row = (int64_t)b * a.V + v;
+    float x[E], raw[E], p[E];
+    load_row<G, E>(a, row, g, x, raw, false);
+    float S, lse, H;
+    row_stats<G, E>(x, g, a.A, p, S, lse, H);
+    const int act = a.action[row];
+    const uint32_t *mb = a.bits ? a.bits + row * a.W : nullptr;
+    float *d = a.dlogits + row * a.A;
+    const float inv = 1.0f / S;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+      int j = g + G * e;
+      if (j < a.A) {
+        bool masked = mb && ((mb[j >> 5] >> (j & 31)) & 1u);
+        float q = p[e] * inv;
+        float l = x[e] - lse;
+        float gj = glp * ((j == act ? 1.f : 0.f) - q);
+        if (q > 0.f) gj -= gen * q * (l + H);
+        d[j] = masked ? 0.f : gj;
+      }
+    }
+  }
+}
+
+// PPOAgent.update GAE (ppo.py:232-243): one lane per env column, reverse scan
+// over T; f32 as the reference's rewards_batch / values.
+__global__ void k_gae(int T, int N, const float *r, const float *d, const float *v,
+                      const float *nv, float gamma, float lam, float *adv, float *ret) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float g = 0.f;
+  for (int t = T - 1; t >= 0; t--) {
+    int64_t i = (int64_t)t * N + n;
+    float nd = 1.f - d[i];
+    float delta = r[i] + nd * gamma * nv[i] - v[i];
+    g = delta + nd * gamma * lam * g;
+    adv[i] = g;
+    ret[i] = g + v[i];
+  }
+}
+
+}  // namespace vmp
+
+// ------------------------------------------------------------ host dispatch
+namespace {
+using namespace vmp;
+
+// groups of G lanes, E elements per lane: smallest G with A <= 16 G, then the
+// smallest E in {4, 8, 16} covering ceil(A / G).
+int pick_g(int A) { return A <= 64 ? 4 : (A <= 256 ? 16 : 64); }
+int pick_e(int A, int G) {
+  int need = (A + G - 1) / G;
+  return need <= 4 ? 4 : (need <= 8 ? 8 : 16);
+}
+int block_threads(int V, int G) {
+  int t = V * G;
+  if (t <= 64) return 64;
+  if (t <= 128) return 128;
+  return 256;
+}
+
+#define VMP_HEAD_CASE(KERN, GG, EE)                                                      \
+  if (G == GG && E == EE) {                                                              \
+    hipLaunchKernelGGL((KERN<GG, EE>), dim3(a.B), dim3(block_threads(a.V, GG)), 0, st, a); \
+    return hipGetLastError();                                                            \
+  }
+#define VMP_HEAD_ALL(KERN)                                                               \
+  VMP_HEAD_CASE(KERN, 4, 4) VMP_HEAD_CASE(KERN, 4, 8) VMP_HEAD_CASE(KERN, 4, 16)         \
+  VMP_HEAD_CASE(KERN, 16, 4) VMP_HEAD_CASE(KERN, 16, 8) VMP_HEAD_CASE(KERN, 16, 16)      \
+  VMP_HEAD_CASE(KERN, 64, 4) VMP_HEAD_CASE(KERN, 64, 8) VMP_HEAD_CASE(KERN, 64, 16)
+
+hipError_t launch_fwd(const HeadArgs &a, hipStream_t st) {
+  const int G = pick_g(a.A), E = pick_e(a.A, G);
+  VMP_HEAD_ALL(k_head_fwd)
+  return hipErrorInvalidValue;
+}
+hipError_t launch_bwd(const HeadArgs &a, hipStream_t st) {
+  const int G = pick_g(a.A), E = pick_e(a.A, G);
+  VMP_HEAD_ALL(k_head_bwd)
+  return hipErrorInvalidValue;
+}
+}  // namespace
+
+namespace vmp {
+// shared with vmp_capi.cpp's vmp_last_error()
+int policy_fail(int code, const char *msg);
+}
+
+extern "C" {
+
+int vmp_policy_head(int32_t B, int32_t V, int32_t A, int32_t mode, const float *logits,
+                    const uint32_t *mask_bits, float wait_ratio, int32_t wait_index,
+                    uint64_t seed, uint64_t offset, int32_t *action, float *logprob,
+                    float *entropy, void *stream) {
+  if (B < 0 || V < 1 || A < 1 || A > VMP_HEAD_MAX_A || !logits || !action)
+    return vmp::policy_fail(VMP_EINVAL, "vmp_policy_head: bad shape or null pointer");
+  if (mode != VMP_HEAD_SAMPLE && mode != VMP_HEAD_GIVEN && mode != VMP_HEAD_ARGMAX)
+    return vmp::policy_fail(VMP_EINVAL, "vmp_policy_head: unknown mode");
+  if (wait_ratio >= 0.f && (!mask_bits || wait_index < 0 || wait_index >= A))
+    return vmp::policy_fail(VMP_EINVAL, "vmp_policy_head: WAIT coin flips need the mask and 0 <= wait_index < A");
+  if (B == 0) return VMP_OK;
+  HeadArgs a{};
+  a.B = B, a.V = V, a.A = A, a.W = (A + 31) / 32, a.mode = mode, a.wait_index = wait_index;
+  a.wait_ratio = wait_ratio, a.seed = seed, a.offset = offset;
+  a.logits = logits, a.bits = mask_bits, a.action = action, a.logprob = logprob,
+  a.entropy = entropy;
+  hipError_t e = launch_fwd(a, (hipStream_t)stream);
+  if (e != hipSuccess) return vmp::policy_fail(VMP_EDEVICE, hipGetErrorString(e));
+  return VMP_OK;
+}
+
+int vmp_policy_head_backward(int32_t B, int32_t V, int32_t A, const float *logits,
+                             const uint32_t *mask_bits, const int32_t *action,
+                             const float *g_logprob, const float *g_entropy, float *dlogits,
+                             void *stream) {
+  if (B < 0 || V < 1 || A < 1 || A > VMP_HEAD_MAX_A || !logits || !action || !dlogits)
+    return vmp::policy_fail(VMP_EINVAL, "vmp_policy_head_backward: bad shape or null pointer");
+  if (B == 0) return VMP_OK;
+  HeadArgs a{};
+  a.B = B, a.V = V, a.A = A, a.W = (A + 31) / 32, a.mode = VMP_HEAD_GIVEN, a.wait_index = -1;
+  a.wait_ratio = -1.f;
+  a.logits = logits, a.bits = mask_bits, a.action = const_cast<int32_t *>(action);
+  a.g_logprob = g_logprob, a.g_entropy = g_entropy, a.dlogits = dlogits;
+  hipError_t e = launch_bwd(a, (hipStream_t)stream);
+  if (e != hipSuccess) return vmp::policy_fail(VMP_EDEVICE, hipGetErrorString(e));
+  return VMP_OK;
+}
+
+int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const float *value,
+            const float *next_value, float gamma, float lam, float *adv, float *ret,
+            void *stream) {
+  if (T < 0 || N < 0 || !reward || !done || !value || !next_value || !adv || !ret)
+    return vmp::policy_fail(VMP_EINVAL, "bad gae arguments");
+  if (T == 0 || N == 0) return VMP_OK;
+  hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, T, N,
+                     reward, done, value, next_value, gamma, lam, adv, ret);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return vmp::policy_fail(VMP_EDEVICE, hipGetErrorString(e));
+  return VMP_OK;
+}
+
+}  // extern "C"

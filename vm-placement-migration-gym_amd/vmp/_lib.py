@@ -16,7 +16,7 @@ EXPORTS = (
     "vmp_set_eval", "vmp_dims", "vmp_reset", "vmp_step", "vmp_heuristic_act",
     "vmp_heuristic_step", "vmp_rollout_heuristic", "vmp_mask", "vmp_mask_bool", "vmp_get_obs",
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
-    "vmp_masked_sample", "vmp_debug_stamps",
+    "vmp_policy_head", "vmp_policy_head_backward", "vmp_debug_stamps",
 )
 
 
@@ -82,13 +82,15 @@ def lib():
         "vmp_get_state": (ctypes.c_int, [P, P, P, P, P, P, P]),
         "vmp_get_rank": (ctypes.c_int, [P, P]),
         "vmp_gae": (ctypes.c_int, [i32, i32, P, P, P, P, f32, f32, P, P, P]),
-        "vmp_masked_sample": (ctypes.c_int, [i32, i32, i32, P, P, u64, u64, P, P, P, P]),
+        "vmp_policy_head": (ctypes.c_int, [i32, i32, i32, i32, P, P, f32, i32, u64, u64, P, P, P,
+                                            P]),
+        "vmp_policy_head_backward": (ctypes.c_int, [i32, i32, i32, P, P, P, P, P, P, P]),
         "vmp_debug_stamps": (ctypes.c_int, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 1:
+    if L.vmp_abi_version() != 2:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

@@ -146,10 +146,12 @@ class BatchedVmEnv:
                                           ptr(done_count)))
         return rewards, done_count
 
-    def mask_bits(self):
+    def mask_bits(self, out=None):
         """Bit-packed invalid-action mask u32 [N, V, ceil(A/32)] (bit set = invalid)."""
         h = self._bind()
-        b = self._empty((self.n_envs, self.V, self.W), torch.int32)
+        b = self._empty((self.n_envs, self.V, self.W), torch.int32) if out is None else out
+        if b.shape != (self.n_envs, self.V, self.W) or b.dtype != torch.int32 or not b.is_contiguous():
+            raise ValueError("mask_bits out must be contiguous int32 [N, V, W]")
         check(lib().vmp_mask(h, ptr(b)))
         return b
 

@@ -1,0 +1,143 @@
+"""Actor head and advantage scan of the PPO path on libvmp.so (HIP, gfx950).
+
+Reference (src/agents/ppo.py):
+  Network.get_action      ppo.py:115-126  masked multi-Categorical: mask to -1e7,
+                                          split into V Categoricals of A, sample /
+                                          log_prob / entropy summed over V
+  Network.get_det_action  ppo.py:128-131  argmax of the unmasked [V, A] logits
+  PPOAgent.act            ppo.py:154-156  WAIT coin flips with migration_ratio
+  PPOAgent.update (GAE)   ppo.py:232-243  reverse scan
+
+`MaskedHead` is the autograd op: forward = vmp_policy_head, backward =
+vmp_policy_head_backward, so the [B, V*A] logits are read once per pass and no
+[V] list of Categorical objects or per-VM multinomial launches exist. Masks
+travel bit-packed (u32 [B, V, ceil(A/32)], what vmp_mask writes); the
+reference's bool [B, V, A] layout is packed on the device by `pack_mask`.
+"""
+import ctypes
+
+import torch
+
+from ._lib import check, lib, ptr
+
+HEAD_SAMPLE, HEAD_GIVEN, HEAD_ARGMAX = 0, 1, 2
+HEAD_MAX_A = 1024
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _need_device(t, what):
+    if not t.is_cuda:
+        raise RuntimeError(f"{what}: the policy head runs on the MI355X (libvmp.so); got a "
+                           f"{t.device} tensor and there is no CPU fallback")
+
+
+def pack_mask(invalid_mask, V, A):
+    """bool invalid mask [..., V, A] or [..., V*A] -> int32 bits [B, V, W]
+    (bit a of word a//32 set = invalid). int32 [B, V, W] passes through."""
+    W = (A + 31) // 32
+    m = invalid_mask
+    if m.dtype == torch.int32 and m.shape[-1] == W:
+        return m.reshape(-1, V, W).contiguous()
+    m = m.reshape(-1, V, A).to(torch.bool)
+    pad = W * 32 - A
+    if pad:
+        m = torch.nn.functional.pad(m, (0, pad))
+    w = m.reshape(m.shape[0], V, W, 32).to(torch.int64)
+    shifts = torch.arange(32, device=m.device, dtype=torch.int64)
+    bits = (w << shifts).sum(-1)
+    return torch.where(bits >= 2**31, bits - 2**32, bits).to(torch.int32).contiguous()
+
+
+class HeadRng:
+    """Counter-based sampling stream: (seed, offset) advanced by B*V per call,
+    so every (sample, VM) draw of a run is distinct and reproducible."""
+
+    def __init__(self, seed: int):
+        self.seed = int(seed) & (2**64 - 1)
+        self.offset = 0
+
+    def take(self, n):
+        o = self.offset
+        self.offset += int(n)
+        return self.seed, o
+
+
+class MaskedHead(torch.autograd.Function):
+    """(logits [B, V*A], bits|None, action|None) -> (action i32 [B,V], logprob [B], entropy [B])."""
+
+    @staticmethod
+    def forward(ctx, logits, bits, action, V, A, rng_seed, rng_offset, wait_ratio, wait_index):
+        _need_device(logits, "MaskedHead")
+        B = logits.shape[0]
+        if logits.dtype != torch.float32:
+            logits = logits.float()
+        logits = logits.contiguous()
+        if logits.numel() != B * V * A:
+            raise ValueError(f"logits {tuple(logits.shape)} do not hold {V} x {A} per sample")
+        if bits is not None and tuple(bits.shape) != (B, V, (A + 31) // 32):
+            raise ValueError(f"mask bits {tuple(bits.shape)} != {(B, V, (A + 31) // 32)}")
+        if action is None:
+            mode = HEAD_SAMPLE
+            act = torch.empty((B, V), dtype=torch.int32, device=logits.device)
+        else:
+            mode = HEAD_GIVEN
+            act = action.to(device=logits.device, dtype=torch.int32).reshape(B, V).contiguous()
+        lp = torch.empty((B,), dtype=torch.float32, device=logits.device)
+        ent = torch.empty((B,), dtype=torch.float32, device=logits.device)
+        check(lib().vmp_policy_head(B, V, A, mode, ptr(logits), ptr(bits), float(wait_ratio),
+                                    int(wait_index), rng_seed, rng_offset, ptr(act), ptr(lp),
+                                    ptr(ent), _stream(logits)))
+        ctx.save_for_backward(logits, bits, act)
+        ctx.V, ctx.A = V, A
+        ctx.mark_non_differentiable(act)
+        return act, lp, ent
+
+    @staticmethod
+    def backward(ctx, g_act, g_lp, g_ent):
+        logits, bits, act = ctx.saved_tensors
+        B = logits.shape[0]
+        d = torch.empty_like(logits)
+        glp = None if g_lp is None else g_lp.float().contiguous()
+        gen = None if g_ent is None else g_ent.float().contiguous()
+        check(lib().vmp_policy_head_backward(B, ctx.V, ctx.A, ptr(logits), ptr(bits), ptr(act),
+                                             ptr(glp), ptr(gen), ptr(d), _stream(logits)))
+        return d, None, None, None, None, None, None, None, None
+
+
+def policy_head(logits, V, A, bits=None, action=None, rng: HeadRng = None, wait_ratio=-1.0,
+                wait_index=-1):
+    """Functional form of MaskedHead (differentiable in logits)."""
+    if A > HEAD_MAX_A:
+        raise ValueError(f"action_dim {A} > {HEAD_MAX_A}")
+    if action is None and rng is None:
+        raise ValueError("sampling needs a HeadRng")
+    if wait_ratio >= 0 and torch.is_grad_enabled() and logits.requires_grad:
+        raise ValueError("WAIT coin flips (PPOAgent.act) are inference-only")
+    seed, off = rng.take(logits.shape[0] * V) if rng is not None else (0, 0)
+    return MaskedHead.apply(logits, bits, action, V, A, seed, off, wait_ratio, wait_index)
+
+
+def det_action(logits, V, A):
+    """get_det_action (ppo.py:128-131): unmasked argmax per VM row -> int32 [B, V]."""
+    _need_device(logits, "det_action")
+    logits = logits.float().contiguous()
+    B = logits.shape[0]
+    act = torch.empty((B, V), dtype=torch.int32, device=logits.device)
+    check(lib().vmp_policy_head(B, V, A, HEAD_ARGMAX, ptr(logits), None, -1.0, -1, 0, 0,
+                                ptr(act), None, None, _stream(logits)))
+    return act
+
+
+def gae(reward, done, value, next_value, gamma, lam):
+    """GAE over [T, N] f32 tensors (ppo.py:232-243) -> (advantages, returns)."""
+    _need_device(reward, "gae")
+    T, N = reward.shape
+    r, d = reward.float().contiguous(), done.float().contiguous()
+    v, nv = value.float().contiguous(), next_value.float().contiguous()
+    adv, ret = torch.empty_like(r), torch.empty_like(r)
+    check(lib().vmp_gae(T, N, ptr(r), ptr(d), ptr(v), ptr(nv), float(gamma), float(lam),
+                        ptr(adv), ptr(ret), _stream(r)))
+    return adv, ret

@@ -1,0 +1,509 @@
+"""PPO on the MI355X env path: the reference's Network / PPOAgent surface
+(src/agents/ppo.py:13-295) over a batched, device-resident rollout.
+
+  PPOConfig          ppo.py:13-34   same fields and defaults (+ build options)
+  ortho_init         ppo.py:86-89
+  Network            ppo.py:91-131  same module tree and state_dict keys; the
+                                    masked multi-Categorical head is the HIP op
+                                    of vmp.head (one pass over the logits)
+  PPOAgent.act       ppo.py:151-161 (mask from vmp_mask, WAIT coin flips drawn
+                                    from numpy's global stream as the reference)
+  PPOAgent.learn     ppo.py:172-226 -> PPOTrainer over all envs of a BatchedVmEnv
+  PPOAgent.update    ppo.py:229-295 (same signature, N = 1)
+  save/load_model    ppo.py:163-170 (`_orig_mod.` keys of the compiled model)
+
+PPOTrainer is the data-parallel batched form of learn/update: each of N envs
+contributes a column of the [T = batch_size, N] rollout, minibatch j is time
+slice [j*mb, (j+1)*mb) of every env (the reference's sequential sampler,
+ppo.py:250-252), advantage normalisation and the KL early stop use the whole
+minibatch, and the update is chunked over envs so the [samples, V*A] logits
+never exceed `chunk_bytes`. With torch.distributed initialised (one process per
+GPU, RCCL), envs are sharded over ranks and each optimizer step all-reduces the
+flat gradient once; AdamW then runs redundantly on every rank.
+
+Reference quirks kept: the value loss broadcasts [mb, 1]
+against [mb] (ppo.py:266-270, a per-env [mb, mb] mean here;
+`value_loss_broadcast=False` gives the elementwise loss), the KL break
+leaves only the current epoch, AdamW's default weight decay 0.01, and learn()
+runs `episodes` episodes (the reference loops training_steps and raises
+IndexError past `episodes`).
+"""
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import head as H
+from .agents import Base, batched_env
+
+
+@dataclass
+class PPOConfig:
+    episodes: int = 2000
+    hidden_size: int = 256
+    migration_ratio: float = 0.5
+    masked: bool = True
+    lr: float = 5e-5
+    gamma: float = 0.99
+    lamda: float = 0.98
+    ent_coef: float = 0.01
+    vf_coef: float = 0.5
+    vf_loss_clip: bool = True
+    k_epochs: int = 4
+    kl_max: float = 0.02
+    eps_clip: float = 0.1
+    max_grad_norm: float = 0.5
+    batch_size: int = 100
+    minibatch_size: int = 25
+    det: bool = False
+    network_arch: str = "separate"
+    reward_scaling: bool = False
+    training_progress_bar: bool = True
+    device: str = "cpu"  # the reference's default; the build always uses the env's GPU
+    # ---- build options (not in the reference) ----
+    value_loss_broadcast: bool = True  # ppo.py:266-270 [mb,1]-[mb] broadcast
+    chunk_bytes: int = 4 << 30         # logits budget per update chunk
+    seed_stride: int = 4               # env/episode reset seed spacing
+
+
+def ortho_init(layer, scale=np.sqrt(2)):
+    nn.init.orthogonal_(layer.weight, gain=scale)
+    nn.init.constant_(layer.bias, 0)
+    return layer
+
+
+def _nvec(action_space):
+    nvec = np.asarray(getattr(action_space, "nvec", action_space), dtype=np.int64)
+    if nvec.ndim != 1 or not np.all(nvec == nvec[0]):
+        raise ValueError("the VmEnv action space is MultiDiscrete([A] * V)")
+    return nvec
+
+
+class Network(nn.Module):
+    """ppo.py:91-131. `head` defaults to the HIP op (vmp.head.policy_head); a
+    callable with the same signature can be injected (tests use a torch
+    reference of the op to exercise the update logic on CPU)."""
+
+    def __init__(self, input_size: int, action_space, hidden_size: int,
+                 dtype: torch.dtype = torch.float32, head=None, seed=None):
+        super().__init__()
+        self.action_nvec = _nvec(action_space)
+        self.V, self.A = int(self.action_nvec.size), int(self.action_nvec[0])
+        self.critic = nn.Sequential(
+            ortho_init(nn.Linear(input_size, hidden_size, dtype=dtype)), nn.Tanh(),
+            ortho_init(nn.Linear(hidden_size, hidden_size, dtype=dtype)), nn.Tanh(),
+            ortho_init(nn.Linear(hidden_size, 1, dtype=dtype), scale=1))
+        self.actor = nn.Sequential(
+            ortho_init(nn.Linear(input_size, hidden_size, dtype=dtype)), nn.Tanh(),
+            ortho_init(nn.Linear(hidden_size, hidden_size, dtype=dtype)), nn.Tanh(),
+            ortho_init(nn.Linear(hidden_size, int(self.action_nvec.sum()), dtype=dtype),
+                       scale=0.01))
+        self._head = head if head is not None else H.policy_head
+        self.rng = H.HeadRng(torch.initial_seed() if seed is None else seed)
+
+    def get_value(self, obs):
+        return self.critic(obs)
+
+    def head(self, logits, invalid_mask=None, action=None, wait_ratio=-1.0, wait_index=-1):
+        """Masked head on precomputed logits -> (action int32 [B,V], logprob [B], entropy [B])."""
+        bits = None if invalid_mask is None else H.pack_mask(invalid_mask, self.V, self.A)
+        return self._head(logits, self.V, self.A, bits=bits, action=action, rng=self.rng,
+                          wait_ratio=wait_ratio, wait_index=wait_index)
+
+    def get_action(self, obs, action=None, invalid_mask=None):
+        """ppo.py:115-126 -> (action int64 [B,V], logprob [B], entropy [B])."""
+        logits = self.actor(obs)
+        act, lp, ent = self.head(logits, invalid_mask, action)
+        return act.long(), lp, ent
+
+    def get_det_action(self, obs, action=None):
+        """ppo.py:128-131: argmax of the unmasked logits; [V] for one observation."""
+        logits = self.actor(obs)
+        a = H.det_action(logits, self.V, self.A).long()
+        return a[0] if obs.dim() == 1 or obs.shape[0] == 1 else a
+
+
+def strip_compiled_prefix(sd):
+    return {k.replace("_orig_mod.", "", 1) if k.startswith("_orig_mod.") else k: v
+            for k, v in sd.items()}
+
+
+class PPOAgent(Base):
+    def __init__(self, env, config: PPOConfig, head=None, gae=None):
+        super().__init__(type(self).__name__, env, config)
+        self.benv = batched_env(env)
+        self.device = self.benv.device
+        self._head_impl = head  # default: the HIP head (vmp.head.policy_head)
+        self._gae_impl = gae    # default: the HIP scan (vmp.head.gae)
+        self.init_model()
+
+    def init_model(self):
+        self.float_dtype = torch.float32
+        self.obs_dim = self.benv.D
+        nvec = np.full(self.benv.V, self.benv.A, dtype=np.int64)
+        self.model = Network(self.obs_dim, nvec, self.config.hidden_size, self.float_dtype,
+                             head=self._head_impl).to(self.device)
+        self.optimizer = torch.optim.AdamW(self.model.parameters(), lr=self.config.lr)
+
+    def eval(self, mode=True):
+        self.model.train(not mode)
+
+    # ---------------------------------------------------------------- act
+    def _coin_flip_bits(self, bits):
+        """ppo.py:153-156 on one env's mask bits (host copy, V x W words): numpy's
+        global stream is consumed exactly as the reference does (one rand()
+        per qualifying row, in row order)."""
+        P, A = self.benv.P, self.benv.A
+        words = bits.cpu().numpy().astype(np.uint32).reshape(self.benv.V, -1)
+        full = np.unpackbits(words.view(np.uint8), axis=1, bitorder="little")[:, :A]
+        out = words.copy()
+        for row in range(self.benv.V):
+            if (np.count_nonzero(full[row]) > 1 and not full[row, P]
+                    and np.random.rand() > self.config.migration_ratio):
+                out[row, P >> 5] |= np.uint32(1 << (P & 31))
+        return torch.from_numpy(out.view(np.int32)).to(self.device).reshape(bits.shape)
+
+    def act(self, obs):
+        """Action for one env (numpy int64 [V]); for a BatchedVmEnv use act_batch."""
+        with torch.no_grad():
+            o = torch.as_tensor(np.asarray(obs), dtype=self.float_dtype,
+                                device=self.device).reshape(1, -1)
+            if self.config.det:
+                return self.model.get_det_action(o).flatten().cpu().numpy()
+            bits = None
+            if self.config.masked:
+                bits = self._coin_flip_bits(self.benv.mask_bits()[:1])
+            act, _, _ = self.model.head(self.model.actor(o), bits)
+            return act.flatten().long().cpu().numpy()
+
+    def act_batch(self, obs, bits=None):
+        """PPOAgent.act for every env of the batch on the device: int32 [N, V].
+        The WAIT coin flips use the head's counter-based stream."""
+        with torch.no_grad():
+            logits = self.model.actor(obs)
+            if self.config.det:
+                return H.det_action(logits, self.benv.V, self.benv.A)
+            if self.config.masked and bits is None:
+                bits = self.benv.mask_bits()
+            ratio = float(self.config.migration_ratio) if self.config.masked else -1.0
+            act, _, _ = self.model._head(logits, self.benv.V, self.benv.A, bits=bits,
+                                         rng=self.model.rng, wait_ratio=ratio,
+                                         wait_index=self.benv.P)
+            return act
+
+    # ------------------------------------------------------------ weights
+    def save_model(self, modelpath):
+        """ppo.py:163-166: keys carry the torch.compile `_orig_mod.` prefix, so the
+        reference's load_model reads the file."""
+        if modelpath:
+            parent = os.path.dirname(modelpath)
+            if parent:
+                os.makedirs(parent, exist_ok=True)
+            sd = {"_orig_mod." + k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+            torch.save(sd, modelpath)
+
+    def load_model(self, modelpath):
+        """ppo.py:168-170; accepts compiled (`_orig_mod.`) and plain state dicts."""
+        sd = torch.load(modelpath, map_location="cpu", weights_only=True)
+        self.model.load_state_dict(strip_compiled_prefix(sd))
+        self.model.eval()
+
+    # ------------------------------------------------------------ training
+    def trainer(self, group=None):
+        if getattr(self, "_trainer", None) is None:
+            self._trainer = PPOTrainer(self, group=group)
+        return self._trainer
+
+    def learn(self):
+        """ppo.py:172-226 over every env of the (batched) env; see PPOTrainer."""
+        return self.trainer().learn()
+
+    def update(self, invalid_mask_batch, action_batch, obs_batch, next_obs_batch, logprob_batch,
+               rewards_batch, done_batch):
+        """ppo.py:229-295 on one env's batch (leading dim = batch_size)."""
+        tr = PPOTrainer(self, group=None, allocate=False, distributed=False)
+        dev = self.device
+        T = obs_batch.shape[0]
+        obs = obs_batch.to(dev, torch.float32).reshape(T, 1, -1)
+        nobs = next_obs_batch.to(dev, torch.float32).reshape(T, 1, -1)
+        bits = H.pack_mask(invalid_mask_batch.to(dev), self.benv.V, self.benv.A).reshape(
+            T, 1, self.benv.V, -1)
+        act = action_batch.to(dev).to(torch.int32).reshape(T, 1, -1)
+        lp = logprob_batch.to(dev, torch.float32).reshape(T, 1)
+        rew = rewards_batch.to(dev, torch.float32).reshape(T, 1)
+        done = done_batch.to(dev).to(torch.float32).reshape(T, 1)
+        with torch.no_grad():
+            values = self.model.get_value(obs.reshape(T, -1)).reshape(T, 1)
+            next_values = self.model.get_value(nobs.reshape(T, -1)).reshape(T, 1)
+        return tr.update_from(obs, bits, act, lp, rew, done, values, next_values)
+
+
+class PPOTrainer:
+    """Batched PPO (rollout + update) over all envs of the agent's BatchedVmEnv."""
+
+    def __init__(self, agent: PPOAgent, group=None, allocate=True, distributed=True):
+        import torch.distributed as dist
+        self.agent, self.cfg = agent, agent.config
+        self.env, self.model = agent.benv, agent.model
+        self.gae = agent._gae_impl if agent._gae_impl is not None else H.gae
+        use = distributed and dist.is_available() and dist.is_initialized()
+        self.dist = dist if use else None
+        self.group = group
+        self.world = self.dist.get_world_size(group) if self.dist else 1
+        self.rank = self.dist.get_rank(group) if self.dist else 0
+        e = self.env
+        self.N, self.V, self.A, self.D, self.W = e.n_envs, e.V, e.A, e.D, e.W
+        self.T = int(self.cfg.batch_size)
+        self.dev = e.device
+        self.episode = 0
+        self.ep_t = 0
+        self.ep_returns = []
+        self.stats = {}
+        if self.dist and allocate:
+            self._sync_params()
+        if allocate:
+            T, N = self.T, self.N
+            f = dict(device=self.dev)
+            self.obs = torch.empty((T, N, self.D), dtype=torch.float32, **f)
+            self.last_obs = torch.empty((N, self.D), dtype=torch.float32, **f)
+            self.bits = (torch.empty((T, N, self.V, self.W), dtype=torch.int32, **f)
+                         if self.cfg.masked else None)
+            self.act = torch.empty((T, N, self.V), dtype=torch.int32, **f)
+            self.logp = torch.empty((T, N), dtype=torch.float32, **f)
+            self.rew = torch.empty((T, N), dtype=torch.float32, **f)
+            self.done = torch.zeros((T, N), dtype=torch.float32, **f)
+            self.r64 = torch.empty((N,), dtype=torch.float64, **f)
+            self.d8 = torch.empty((N,), dtype=torch.uint8, **f)
+            self.ep_ret = torch.zeros((N,), dtype=torch.float64, **f)
+            if self.cfg.reward_scaling:
+                self.rs_R = torch.zeros((N,), dtype=torch.float64, **f)
+                self.rs_n = 0
+                self.rs_mean = torch.zeros((N,), dtype=torch.float64, **f)
+                self.rs_S = torch.zeros((N,), dtype=torch.float64, **f)
+                self.rs_std = torch.zeros((N,), dtype=torch.float64, **f)
+            self._started = False
+
+    # ------------------------------------------------------------ plumbing
+    def _sync_params(self):
+        for p in self.model.parameters():
+            self.dist.broadcast(p.data, src=0, group=self.group)
+
+    def _allreduce(self, t):
+        if self.dist:
+            self.dist.all_reduce(t, group=self.group)
+        return t
+
+    def _episode_seeds(self, episode):
+        """reset seed of env i in `episode`: seed + stride*(episode*N_global + global i)
+        (disjoint PCG64 streams for every env and episode; the reference uses
+        seed + i_episode for its single env, ppo.py:192)."""
+        n_glob = self.N * self.world
+        gi = self.rank * self.N + torch.arange(self.N, device=self.dev, dtype=torch.int64)
+        return int(self.env.config.seed) + int(self.cfg.seed_stride) * (episode * n_glob + gi)
+
+    def _start_episode(self, out_obs):
+        self.env.eval(False)
+        out_obs.copy_(self.env.reset(self._episode_seeds(self.episode)))
+        self.ep_t = 0
+        self.ep_ret.zero_()
+
+    def _scale_reward(self, r):
+        """RewardScaler (ppo.py:55-68) per env: R = gamma R + r, running std of R
+        (the reference's RunningMeanStd, incl. std = x at n = 1)."""
+        self.rs_R.mul_(self.cfg.gamma).add_(r)
+        self.rs_n += 1
+        x = self.rs_R
+        if self.rs_n == 1:
+            self.rs_mean.copy_(x)
+            self.rs_std.copy_(x)
+        else:
+            old = self.rs_mean.clone()
+            self.rs_mean.add_((x - old) / self.rs_n)
+            self.rs_S.add_((x - old) * (x - self.rs_mean))
+            self.rs_std.copy_(torch.sqrt(self.rs_S / self.rs_n))
+        return r / (self.rs_std + 1e-8)
+
+    # ------------------------------------------------------------ rollout
+    @torch.no_grad()
+    def collect(self):
+        """batch_size steps of every env (ppo.py:194-217): mask, sample, step."""
+        T, cfg, env, m = self.T, self.cfg, self.env, self.model
+        ep_len = int(env.config.training_steps)
+        if not self._started:
+            self._start_episode(self.obs[0])
+            self._started = True
+        else:
+            self.obs[0].copy_(self.last_obs)
+        for t in range(T):
+            o = self.obs[t]
+            bits = None
+            if self.bits is not None:
+                bits = env.mask_bits(out=self.bits[t])
+            logits = m.actor(o)
+            act, lp, _ = m._head(logits, self.V, self.A, bits=bits, rng=m.rng)
+            self.act[t].copy_(act)
+            self.logp[t].copy_(lp)
+            nxt = self.obs[t + 1] if t + 1 < T else self.last_obs
+            env.step(act, obs=nxt, reward=self.r64, done=self.d8, want_valid=False)
+            self.ep_ret.add_(self.r64)
+            r = self._scale_reward(self.r64) if cfg.reward_scaling else self.r64
+            self.rew[t].copy_(r)
+            self.ep_t += 1
+            if self.ep_t >= ep_len:
+                # every env terminates together (timestep >= training_steps, env.py:160-163)
+                self.done[t].fill_(1.0)
+                self._end_episode()
+                self.episode += 1
+                self._start_episode(nxt)
+            else:
+                self.done[t].zero_()
+        self.agent.total_steps += T * self.N
+
+    def _end_episode(self):
+        rets = self.ep_ret.clone()
+        if self.dist:
+            parts = [torch.empty_like(rets) for _ in range(self.world)]
+            self.dist.all_gather(parts, rets, group=self.group)
+            rets = torch.cat(parts)
+        self.ep_returns.append(rets.cpu().numpy())
+
+    # ------------------------------------------------------------- update
+    @torch.no_grad()
+    def _values(self, obs):
+        T, N = obs.shape[:2]
+        flat = obs.reshape(T * N, -1)
+        out = torch.empty((T * N,), dtype=torch.float32, device=obs.device)
+        step = 1 << 16
+        for i in range(0, T * N, step):
+            out[i:i + step] = self.model.get_value(flat[i:i + step]).flatten()
+        return out.reshape(T, N)
+
+    def update(self):
+        """ppo.py:229-295 on the collected [T, N] rollout."""
+        with torch.no_grad():
+            values = self._values(self.obs)
+            next_values = torch.empty_like(values)
+            next_values[:-1] = values[1:]
+            next_values[-1] = self._values(self.last_obs[None])[0]
+        return self.update_from(self.obs, self.bits, self.act, self.logp, self.rew, self.done,
+                                values, next_values)
+
+    def update_from(self, obs, bits, act, old_lp, rew, done, values, next_values):
+        cfg, m = self.cfg, self.model
+        T, N = rew.shape
+        with torch.no_grad():
+            adv, ret = self.gae(rew, done, values, next_values, cfg.gamma, cfg.lamda)
+        mbs = int(cfg.minibatch_size)
+        n_mb = math.ceil(T / mbs)
+        VA = self.V * self.A
+        eps = cfg.eps_clip
+        params = [p for p in m.parameters()]
+        stats = dict(minibatches=0, kl_breaks=0, clipfracs=[])
+        for epoch in range(cfg.k_epochs):
+            for j in range(n_mb):
+                t0, t1 = j * mbs, min(T, (j + 1) * mbs)
+                mt = t1 - t0
+                m_glob = mt * N * self.world
+                with torch.no_grad():
+                    a_mb = adv[t0:t1]
+                    s = self._allreduce(a_mb.sum().reshape(1).double())
+                    mean = (s / m_glob).float()
+                    ss = self._allreduce(((a_mb - mean) ** 2).sum().reshape(1).double())
+                    std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
+                    adv_n = (a_mb - mean) / (std + 1e-10)
+                ce = max(1, min(N, int(cfg.chunk_bytes) // max(1, mt * VA * 4)))
+                for p in params:
+                    p.grad = None
+                kl_sum = torch.zeros(1, dtype=torch.float64, device=rew.device)
+                clip_n = torch.zeros(1, dtype=torch.float64, device=rew.device)
+                for n0 in range(0, N, ce):
+                    n1 = min(N, n0 + ce)
+                    nc = n1 - n0
+                    o = obs[t0:t1, n0:n1].reshape(mt * nc, -1)
+                    b = None if bits is None else bits[t0:t1, n0:n1].reshape(mt * nc, self.V, -1)
+                    a = act[t0:t1, n0:n1].reshape(mt * nc, self.V)
+                    logits = m.actor(o)
+                    _, newlp, ent = m._head(logits, self.V, self.A, bits=b, action=a,
+                                            rng=m.rng)
+                    newlp = newlp.reshape(mt, nc)
+                    logratio = newlp - old_lp[t0:t1, n0:n1]
+                    ratio = torch.exp(logratio)
+                    kl_sum += logratio.detach().double().sum()
+                    clip_n += ((ratio.detach() - 1.0).abs() > eps).double().sum()
+                    an = adv_n[:, n0:n1]
+                    surr = -ratio * an
+                    surr_c = -torch.clamp(ratio, 1 - eps, 1 + eps) * an
+                    loss_clip = torch.max(surr, surr_c).sum() / m_glob
+                    newv = m.get_value(o).reshape(mt, nc)
+                    R, Vb = ret[t0:t1, n0:n1], values[t0:t1, n0:n1]
+                    if cfg.value_loss_broadcast:
+                        # newvalues [mb,1] - returns [mb] -> [mb, mb] (ppo.py:266-270), per env
+                        du = newv[:, None, :] - R[None, :, :]
+                        vcl = Vb[None, :, :] + torch.clamp(newv[:, None, :] - Vb[None, :, :],
+                                                           -eps, eps)
+                        dc = vcl - R[None, :, :]
+                        denom = mt * mt * N * self.world
+                    else:
+                        du = newv - R
+                        dc = Vb + torch.clamp(newv - Vb, -eps, eps) - R
+                        denom = m_glob
+                    if cfg.vf_loss_clip:
+                        lvf = torch.max(du * du, dc * dc).sum() / denom
+                    else:
+                        lvf = (du * du).sum() / denom
+                    loss = loss_clip - cfg.ent_coef * ent.sum() / m_glob + cfg.vf_coef * 0.5 * lvf
+                    loss.backward()
+                    del logits
+                self._allreduce(kl_sum)
+                kl = float(-kl_sum / m_glob)
+                if kl > cfg.kl_max:  # ppo.py:263-264: leaves this epoch's minibatch loop
+                    for p in params:
+                        p.grad = None
+                    stats["kl_breaks"] += 1
+                    break
+                self._allreduce(clip_n)
+                stats["clipfracs"].append(float(clip_n / m_glob))
+                if self.dist:
+                    self._allreduce_grads(params)
+                nn.utils.clip_grad_norm_(params, cfg.max_grad_norm)
+                self.agent.optimizer.step()
+                stats["minibatches"] += 1
+                stats["kl"] = kl
+        self.stats = stats
+        return stats
+
+    def _allreduce_grads(self, params):
+        """One RCCL all-reduce of the flat gradient."""
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        self.dist.all_reduce(flat, group=self.group)
+        o = 0
+        for p, g in zip(params, grads):
+            n = g.numel()
+            p.grad = flat[o:o + n].view_as(p)
+            o += n
+
+    # ------------------------------------------------------------- driver
+    def train_updates(self, n_updates):
+        for _ in range(int(n_updates)):
+            self.collect()
+            self.update()
+
+    def learn(self):
+        """ppo.py:186-224: `episodes` episodes of training_steps steps per env,
+        one update every batch_size steps (batches straddle episodes)."""
+        total = int(self.cfg.episodes) * int(self.env.config.training_steps)
+        n_updates = total // self.T
+        show = bool(self.cfg.training_progress_bar) and self.rank == 0
+        for u in range(n_updates):
+            self.collect()
+            self.update()
+            if show and self.ep_returns:
+                print("update %d/%d  episodes %d  median return %.3f" %
+                      (u + 1, n_updates, len(self.ep_returns),
+                       float(np.median(self.ep_returns[-1]))), flush=True)
+        return self.ep_returns
+
