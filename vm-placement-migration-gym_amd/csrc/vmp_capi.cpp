@@ -90,6 +90,7 @@ struct vmp_handle {
   uint32_t *scratch_bits;  // for vmp_mask_bool
   PoisConst *pois_dev;
   uint64_t *stamps;
+  uint64_t *jump_dev;
 };
 
 namespace {
@@ -287,6 +288,21 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
     HIP_TRY(hipMalloc(&h->pois_dev, sizeof(pc)));
     HIP_TRY(hipMemcpy(h->pois_dev, pc, sizeof(pc), hipMemcpyHostToDevice));
     p.pois = h->pois_dev;
+    // PCG64 jump table for the lane-parallel draws (k_env prologue)
+    uint64_t jt[64 * 4];
+    const unsigned __int128 a = ((unsigned __int128)0x2360ED051FC65DA4ULL << 64) | 0x4385DF649FCCF645ULL;
+    unsigned __int128 A = a, M = 1;
+    for (int j = 0; j < 64; j++) {
+      jt[4 * j + 0] = (uint64_t)(A >> 64);
+      jt[4 * j + 1] = (uint64_t)A;
+      jt[4 * j + 2] = (uint64_t)(M >> 64);
+      jt[4 * j + 3] = (uint64_t)M;
+      A *= a;
+      M = M * a + 1;
+    }
+    HIP_TRY(hipMalloc(&h->jump_dev, sizeof(jt)));
+    HIP_TRY(hipMemcpy(h->jump_dev, jt, sizeof(jt), hipMemcpyHostToDevice));
+    p.jump = h->jump_dev;
   }
   p.vmw = h->vmw;
   p.pm = h->pm;
@@ -331,6 +347,7 @@ int vmp_destroy(vmp_handle *h) {
   (void)hipFree(h->lg_svc);
   (void)hipFree(h->scratch_bits);
   (void)hipFree(h->pois_dev);
+  (void)hipFree(h->jump_dev);
   (void)hipFree(h->stamps);
   delete h;
   return VMP_OK;

@@ -32,6 +32,13 @@
 
 namespace vmp {
 
+// Streaming stores (obs / state written once per launch, not re-read by it).
+#ifdef VMP_NT_STORE
+#define ST_NT(ptr, val) __builtin_nontemporal_store((val), (ptr))
+#else
+#define ST_NT(ptr, val) (*(ptr) = (val))
+#endif
+
 // ------------------------------------------------------------ wave utils --
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -581,6 +588,7 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
 struct Tables {
   double cent[128];
   float fcent[128];
+  PoisConst pois[2];  // block copy of p.pois, read by the prologue draws
 };
 
 __device__ __forceinline__ int w_pl(uint32_t w) { return (int)(w & 0xFFFFu); }
@@ -761,32 +769,149 @@ __device__ __noinline__ uint32_t svc_fallback(uint64_t LDSP *st, const uint64_t 
   return (uint32_t)(x + 1);
 }
 
-__device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, int K, int V) {
+// Lane-parallel PCG64: lane j of a chunk holds the state after j+1 draws from
+// the chunk's base state, s_j = A_j*base + M_j*inc (jump table p.jump), and
+// its uniform next_double. Draws are consumed in stream order; the committed
+// state after `pos` draws of the chunk is the base (pos = 0) or lane pos-1's.
+struct ParRng {
+  U128 base, inc;  // wave-uniform
+  U128 st;         // lane j: state after j+1 draws of the chunk
+  double u;        // lane j: uniform j of the chunk
+  int pos;         // draws consumed in this chunk (wave-uniform)
+};
+__device__ __forceinline__ U128 rl128(U128 x, int l) {
+  return U128{readlane_u64(x.hi, l), readlane_u64(x.lo, l)};
+}
+__device__ __forceinline__ void par_fill(ParRng &g, const U128 &JA, const U128 &JM) {
+  g.st = add128(mul128(JA, g.base), mul128(JM, g.inc));
+  const uint64_t x = g.st.hi ^ g.st.lo;
+  const unsigned rot = (unsigned)(g.st.hi >> 58);
+  const uint64_t out = (x >> rot) | (x << ((64 - rot) & 63));
+  g.u = (double)(out >> 11) * (1.0 / 9007199254740992.0);
+  g.pos = 0;
+}
+__device__ __forceinline__ void par_next_chunk(ParRng &g, const U128 &JA, const U128 &JM) {
+  g.base = rl128(g.st, 63);
+  par_fill(g, JA, JM);
+}
+__device__ __forceinline__ U128 par_state(const ParRng &g) {
+  return g.pos == 0 ? g.base : rl128(g.st, uni(g.pos - 1));
+}
+
+// random_poisson, mult method (lam < 10): the running product is formed in
+// stream order (same rounding as the sequential loop), uniforms by readlane.
+__device__ __forceinline__ int64_t par_poisson_mult(ParRng &g, double enlam, const U128 &JA,
+                                                    const U128 &JM) {
+  double prod = 1.0;
+  int64_t X = 0;
+#pragma unroll 1
+  for (;;) {
+    if (g.pos == 64) par_next_chunk(g, JA, JM);
+    prod *= readlane_f64(g.u, uni(g.pos));
+    g.pos++;
+    if (prod > enlam)
+      X += 1;
+    else
+      return X;
+  }
+}
+
+// random_poisson_ptrs (lam >= 10): every loop iteration consumes one (U, V)
+// pair and its outcome depends on that pair only, so lanes i < 32 evaluate
+// pair i of the chunk at once; the n-th draw is the n-th accepting pair.
+struct PtrsChunk {
+  uint64_t acc;  // accepting pairs of the chunk
+  int64_t k;     // lane i: k of pair i
+  bool valid;
+};
+__device__ __forceinline__ void par_ptrs_eval(const ParRng &g, const PoisConst &c, PtrsChunk &pc) {
+  const int lane = lane_id();
+  const int i = lane & 31;
+  const double U = __shfl(g.u, 2 * i) - 0.5;
+  const double V = __shfl(g.u, 2 * i + 1);
+  const double us = 0.5 - fabs(U);
+  const int64_t k = (int64_t)floor((2 * c.a / us + c.b) * U + c.lam + 0.43);
+  bool ok;
+  if ((us >= 0.07) && (V <= c.vr))
+    ok = true;
+  else if ((k < 0) || ((us < 0.013) && (V > us)))
+    ok = false;
+  else
+    ok = ptrs_accept(V, us, k, c.lam, c.a, c.b, c.loglam, c.log_invalpha, c.loggam_tab, c.tab_n);
+  pc.acc = ballot(ok && lane < 32);
+  pc.k = k;
+  pc.valid = true;
+}
+__device__ __forceinline__ int64_t par_poisson_ptrs(ParRng &g, const PoisConst &c, PtrsChunk &pc,
+                                                    const U128 &JA, const U128 &JM) {
+#pragma unroll 1
+  for (;;) {
+    if (g.pos == 64) {
+      par_next_chunk(g, JA, JM);
+      pc.valid = false;
+    }
+    if (!pc.valid) par_ptrs_eval(g, c, pc);
+    const uint64_t m = pc.acc & (~0ull << (g.pos >> 1));
+    if (m == 0) {
+      g.pos = 64;
+      continue;
+    }
+    const int i = uni(__builtin_ctzll(m));
+    g.pos = 2 * i + 2;
+    return (int64_t)readlane_u64((uint64_t)pc.k, i);
+  }
+}
+
+__device__ __forceinline__ int64_t par_poisson(ParRng &g, const PoisConst &c, PtrsChunk &pc,
+                                               const U128 &JA, const U128 &JM) {
+  if (c.kind == 0) return 0;  // lam == 0: no draw consumed
+  if (c.kind == 1) return par_poisson_mult(g, c.enlam, JA, JM);
+  return par_poisson_ptrs(g, c, pc, JA, JM);
+}
+
+__device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, const Tables &T,
+                                        int K, int V, const U128 &JA, const U128 &JM) {
   const int lane = lane_id();
   EnvHdr LDSP *H = L.hdr;
+  ParRng g;
+  PtrsChunk pc;
+  pc.valid = false;
+  // K arrival counts, rng3 (env.py:272)
   Pcg r3 = ld_pcg(H, 2);
+  g.base = r3.s;
+  g.inc = r3.inc;
+  par_fill(g, JA, JM);
   int64_t need = 0;
 #pragma unroll 1
   for (int k = 0; k < K; k++) {
-    const int64_t a = poisson(r3, p.pois[0]);
+    const int64_t a = par_poisson(g, T.pois[0], pc, JA, JM);
     if (lane == 0) L.arr[k] = (int32_t)(a < 0x7fffffff ? a : 0x7fffffff);
     need += a < V ? a : V;
   }
+  r3.s = par_state(g);
   st_pcg(H, 2, r3);
+  // up to scap speculative service lengths, rng4 (env.py:289), with the state
+  // after each draw for the commit
   Pcg r4 = ld_pcg(H, 3);
   const int S = (int)(need < p.scap ? need : p.scap);
+  g.base = r4.s;
+  g.inc = r4.inc;
+  pc.valid = false;
+  if (S > 0) par_fill(g, JA, JM);
 #pragma unroll 1
   for (int j = 0; j < S; j++) {
-    const int64_t x = poisson(r4, p.pois[1]);
+    const int64_t x = par_poisson(g, T.pois[1], pc, JA, JM);
+    const U128 sj = par_state(g);
     if (lane == 0) {
       L.svc[j] = (uint32_t)(x + 1);
-      L.svcst[2 * j] = r4.s.hi;
-      L.svcst[2 * j + 1] = r4.s.lo;
+      L.svcst[2 * j] = sj.hi;
+      L.svcst[2 * j + 1] = sj.lo;
     }
   }
+  const U128 fb = S > 0 ? par_state(g) : r4.s;
   if (lane == 0) {
-    L.svcfb[0] = r4.s.hi;  // fallback continues after the last speculative draw
-    L.svcfb[1] = r4.s.lo;
+    L.svcfb[0] = fb.hi;  // fallback continues after the last speculative draw
+    L.svcfb[1] = fb.lo;
     L.svcinfo[0] = S;
     L.svcinfo[1] = 0;  // consumed
   }
@@ -1270,14 +1395,14 @@ __device__ __forceinline__ void write_obs(const EnvParams &p, const Lds &L, cons
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
     if (live(wa[s])) {
-      obs[v] = (float)w_pl(wa[s]);
-      obs[V + v] = T.fcent[w_cc(wa[s])];
-      obs[2 * V + v] = T.fcent[w_cm(wa[s])];
+      ST_NT(obs + v, (float)w_pl(wa[s]));
+      ST_NT(obs + V + v, T.fcent[w_cc(wa[s])]);
+      ST_NT(obs + 2 * V + v, T.fcent[w_cm(wa[s])]);
     }
   }
   for (int i = lane; i < P; i += 64) {
-    obs[3 * V + i] = (float)L.cpu[i];
-    obs[3 * V + P + i] = (float)L.mem[i];
+    ST_NT(obs + 3 * V + i, (float)L.cpu[i]);
+    ST_NT(obs + 3 * V + P + i, (float)L.mem[i]);
   }
 }
 
@@ -1324,15 +1449,10 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
   const uint64_t t_start = __builtin_amdgcn_s_memtime();
   const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
-  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
-    T.cent[i] = (double)i / 100.0;
-    T.fcent[i] = (float)((double)i / 100.0);
-  }
-  __syncthreads();  // the only block-wide barrier: waves are independent below
   const int lane = lane_id();
   const int wid = threadIdx.x >> 6;
-  const int e = uni(blockIdx.x * kWavesPerBlock + wid);
-  if (e >= p.N) return;
+  const int e_raw = uni(blockIdx.x * kWavesPerBlock + wid);
+  const int e = e_raw < p.N ? e_raw : p.N - 1;  // tail waves load a valid env, then leave
   char LDSP *base = (char LDSP *)lds + wid * p.lds_wave_bytes;
   const Lds L = make_lds(p, base);
   const int V = p.V, P = p.P;
@@ -1342,6 +1462,17 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
   // (indices are clamped instead of branched on, so no load is conditional and
   // the waits below can count: a skipped load would force vmcnt(0))
   const uint64_t hv = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane & 31];
+  // Poisson constants for the block's LDS copy (issued before the state loads,
+  // so waiting for them never waits on the state)
+  constexpr int kPoisWords = (int)(2 * sizeof(PoisConst) / 4);
+  const uint32_t pw = reinterpret_cast<const uint32_t *>(p.pois)[threadIdx.x % kPoisWords];
+  // this lane's PCG64 jump entry (lane-parallel draws), right behind the header
+  U128 JA{0, 0}, JM{0, 0};
+  if (o.k_steps > 0) {
+    const uint64_t *jt = p.jump + 4 * lane;
+    JA = U128{jt[0], jt[1]};
+    JM = U128{jt[2], jt[3]};
+  }
   const double *pm = p.pm + (int64_t)e * 2 * P;
   const int n_pm = 2 * P;
   double pv[4];
@@ -1359,19 +1490,30 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
     rem[s] = (uint32_t)(w >> 32);
   }
   __asm__ volatile("" ::: "memory");  // ... and the VM words before any wait
+  // size tables (k/100 in f64 and f32) while the loads are in flight; the only
+  // block-wide barrier: waves are independent below
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+    T.cent[i] = (double)i / 100.0;
+    T.fcent[i] = (float)((double)i / 100.0);
+  }
+  if (threadIdx.x < kPoisWords) reinterpret_cast<uint32_t *>(T.pois)[threadIdx.x] = pw;
+  __syncthreads();
+  if (e_raw >= p.N) return;
   if (lane < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane] = hv;
+  wsync();
+#ifdef VMP_STAMPS
+  const uint64_t t_loaded = __builtin_amdgcn_s_memtime();
+#endif
+  // the draws need only the header: they run while the PM / VM loads land
+  if (o.k_steps > 0) predraw(p, L, T, o.k_steps, V, JA, JM);
+#ifdef VMP_STAMPS
+  const uint64_t t_drawn = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
   for (int j = 0; j < 4; j++)
     if (j * 64 + lane < n_pm) L.cpu[j * 64 + lane] = pv[j];
   for (int i = 256 + lane; i < n_pm; i += 64) L.cpu[i] = pm[i];  // P > 128
   wsync();
-#ifdef VMP_STAMPS
-  const uint64_t t_loaded = __builtin_amdgcn_s_memtime();
-#endif
-  if (o.k_steps > 0) predraw(p, L, o.k_steps, V);
-#ifdef VMP_STAMPS
-  const uint64_t t_drawn = __builtin_amdgcn_s_memtime();
-#endif
   STAMP_DECL
 #ifdef VMP_STAMPS
   st_acc[13] = t_loaded - t_start;
@@ -1421,10 +1563,10 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
       const int v = s * 64 + lane;
-      if (live(wa[s])) vmo[v] = (uint64_t)wa[s] | ((uint64_t)rem[s] << 32);
+      if (live(wa[s])) ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rem[s] << 32));
     }
     double *pmo = p.pm + (int64_t)e * 2 * P;
-    for (int i = lane; i < 2 * P; i += 64) pmo[i] = L.cpu[i];
+    for (int i = lane; i < 2 * P; i += 64) ST_NT(pmo + i, (double)L.cpu[i]);
     if (lane < 32)
       reinterpret_cast<uint64_t *>(p.hdr + e)[lane] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane];
   }
