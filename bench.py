@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--rollout-k", type=int, default=100, help="steps per fused rollout launch")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ppo", action="store_true", help="skip the PPO train / eval legs")
+    ap.add_argument("--ppo-envs", type=int, default=8192, help="PPO training envs per GPU")
+    ap.add_argument("--ppo-eval-envs", type=int, default=4096)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,6 +193,11 @@ def main():
                 traffic = float(tj["bytes_per_launch"])
         except Exception:
             traffic = None
+    env.close()
+    ppo_train = ppo_eval = None
+    if not args.no_ppo:
+        ppo_train = _guard(bench_ppo_train, args, dev, rank, world, dist)
+        ppo_eval = _guard(bench_ppo_eval, args, dev, rank, world, dist)
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / K, "higher_is_better": True,
@@ -207,12 +215,122 @@ def main():
         "cpu_baseline": cpu,
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},
         "parity": parity,
+        "ppo_train": ppo_train,
+        "ppo_eval": ppo_eval,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    env.close()
     if dist:
         dist.destroy_process_group()
+
+
+def _guard(fn, *a):
+    """A secondary leg reports its failure in the JSON instead of ending the run."""
+    try:
+        return fn(*a)
+    except Exception as ex:  # noqa: BLE001
+        return {"error": f"{type(ex).__name__}: {ex}"}
+
+
+def _max_over_ranks(x, dev, dist):
+    if dist:
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        x = float(t[0])
+    return x
+
+
+def bench_ppo_train(args, dev, rank, world, dist):
+    """BASELINE config 3 (config/100.yml, PPO from scratch, reward wr, 8192 envs per
+    GPU): one untimed update, then one timed update = batch_size rollout steps of
+    every env + PPOAgent.update (4 epochs x 4 minibatches), data-parallel over ranks
+    (one RCCL all-reduce of the flat gradient per optimizer step)."""
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import PPOAgent, PPOConfig
+    torch.manual_seed(0)
+    N = args.ppo_envs
+    cfg = Config(pms=100, vms=300, service_length=1000, arrival_rate=1.8182,
+                 training_steps=10000, eval_steps=100000, seed=0, reward_function="wr",
+                 sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
+    env = BatchedVmEnv(cfg, N, seeds=4 * (rank * N + np.arange(N, dtype=np.int64)), device=dev)
+    ag = PPOAgent(env, PPOConfig(hidden_size=512, batch_size=100, minibatch_size=25,
+                                 migration_ratio=0.002, masked=True))
+    tr = ag.trainer()
+    tr.collect()
+    tr.update()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    tr.collect()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    st = tr.update()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t2 = time.perf_counter()
+    total = _max_over_ranks(t2 - t0, dev, dist)
+    steps = world * N * tr.T
+    env.close()
+    return {"value": steps / total, "unit": "env-steps/s", "dtype": "f32",
+            "workload": "config/100.yml (P100 V300), PPO train from scratch, reward wr, "
+                        "hidden 512, batch 100 / minibatch 25, 4 epochs",
+            "envs_per_gpu": N, "global_envs": world * N, "updates_timed": 1,
+            "s_per_update": total, "collect_s": t1 - t0, "update_s": t2 - t1,
+            "minibatch_steps": st["minibatches"], "kl_breaks": st["kl_breaks"],
+            "parallelism": f"data-parallel x{world} (RCCL grad all-reduce)" if world > 1
+            else "single GPU"}
+
+
+def bench_ppo_eval(args, dev, rank, world, dist):
+    """BASELINE config 2: config/10.yml PPO eval with weights-10/ppo-wr.pt (the
+    reference's own weights, tests/golden/ppo10_wr_weights.npz), 4096 batched envs,
+    masked, migration_ratio 0.5 WAIT coin flips: per step mask + actor forward +
+    masked sample + env.step for every env."""
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import PPOAgent, PPOConfig
+    N = args.ppo_eval_envs
+    cfg = Config(pms=10, vms=30, service_length=1000, arrival_rate=0.0182, training_steps=10000,
+                 eval_steps=100000, seed=1, reward_function="wr", sequence="uniform",
+                 cap_target_util=True, beta=0.5, allow_null_action=True)
+    env = BatchedVmEnv(cfg, N, seeds=1 + 4 * (rank * N + np.arange(N, dtype=np.int64)),
+                       device=dev)
+    env.eval(True)
+    ag = PPOAgent(env, PPOConfig(hidden_size=512, masked=True, migration_ratio=0.5))
+    w = np.load(os.path.join(ROOT, "tests", "golden", "ppo10_wr_weights.npz"))
+    ag.model.load_state_dict({k: torch.tensor(w[k]) for k in w.files})
+    ag.eval(True)
+    obs = env.obs()
+    bits = torch.empty((N, env.V, env.W), dtype=torch.int32, device=dev)
+    rew = torch.empty((N,), dtype=torch.float64, device=dev)
+    done = torch.empty((N,), dtype=torch.uint8, device=dev)
+
+    def step():
+        env.mask_bits(out=bits)
+        a = ag.act_batch(obs, bits)
+        env.step(a, obs=obs, reward=rew, done=done, want_valid=False)
+
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    K = 200
+    t0 = time.perf_counter()
+    for _ in range(K):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    env.close()
+    return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f32",
+            "workload": "config/10.yml (P10 V30), PPO eval, weights-10/ppo-wr.pt, masked, "
+                        "migration_ratio 0.5", "envs_per_gpu": N, "steps": K,
+            "ms_per_step": 1e3 * el / K}
 
 
 if __name__ == "__main__":
