@@ -65,6 +65,7 @@ struct HeadArgs {
   float *entropy;        // [B] (nullable)
   const float *g_logprob, *g_entropy;  // backward: dL/dlogprob[B], dL/dentropy[B]
   float *dlogits;        // backward output [B][V][A] (may alias logits)
+  float *row_lp, *row_ent;  // tiled kernels: per-row results [B*V]
 };
 
 // Loads one row into registers with the mask applied and, for SAMPLE/GIVEN,
@@ -285,6 +286,264 @@ __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tiled row kernels (A <= kTileMaxA, the 10.yml / 100.yml shapes): one wave
+// per tile of 64 consecutive (b, v) rows, lane = row. The tile (64*A floats,
+// contiguous in HBM) is copied into LDS with 16-B loads (fully coalesced,
+// every byte read once), then each lane runs its row out of LDS (even A:
+// 8-B ds_read_b64 row reads, conflict-free for A = 102). Row statistics follow
+// Categorical(logits=masked) exactly as the group kernels: lse = m + log S
+// rounded in f32, l_j = x_j - lse, logprob = l_a, entropy = -sum q_j l_j
+// = lse - (sum p_j x_j)/S. Per-row results go to a row buffer; k_rowsum adds
+// them per sample in a fixed order (deterministic).
+constexpr int kTileMaxA = 128;
+
+__device__ __forceinline__ void tile_load(const float *src, float *lds, int n) {
+  const int lane = threadIdx.x & 63;
+  const int n4 = n >> 2;
+  const float4 *s4 = reinterpret_cast<const float4 *>(src);
+  float4 *d4 = reinterpret_cast<float4 *>(lds);
+  for (int i = lane; i < n4; i += 64) d4[i] = s4[i];
+  for (int i = (n4 << 2) + lane; i < n; i += 64) lds[i] = src[i];
+}
+__device__ __forceinline__ void tile_store(float *dst, const float *lds, int n) {
+  const int lane = threadIdx.x & 63;
+  const int n4 = n >> 2;
+  const float4 *s4 = reinterpret_cast<const float4 *>(lds);
+  float4 *d4 = reinterpret_cast<float4 *>(dst);
+  for (int i = lane; i < n4; i += 64) d4[i] = s4[i];
+  for (int i = (n4 << 2) + lane; i < n; i += 64) dst[i] = lds[i];
+}
+
+// Quad layout inside a tile: wave w owns rows 16w..16w+15, lane l works on
+// row 16w + l/4 with the 4 lanes of its quad taking elements j = c + 4k
+// (c = l%4): row reductions are 2 quad shuffles (DPP), per-lane work is A/4.
+__device__ __forceinline__ float qmax(float x) {
+  x = fmaxf(x, __shfl_xor(x, 1));
+  return fmaxf(x, __shfl_xor(x, 2));
+}
+__device__ __forceinline__ float qsum(float x) {
+  x += __shfl_xor(x, 1);
+  return x + __shfl_xor(x, 2);
+}
+
+__device__ __forceinline__ void load_mask_words(const HeadArgs &a, int64_t row, uint32_t (&mw)[4]) {
+#pragma unroll
+  for (int w = 0; w < 4; w++) mw[w] = 0u;
+  if (!a.bits) return;
+  const uint32_t *mb = a.bits + row * a.W;
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+    if (w < a.W) mw[w] = mb[w];
+  const int tail = a.A - 32 * (a.W - 1);  // bits past A are ignored
+#pragma unroll
+  for (int w = 0; w < 4; w++)
+    if (w == a.W - 1 && tail < 32) mw[w] &= (1u << tail) - 1u;
+}
+
+__device__ __forceinline__ bool bit_of(const uint32_t (&mw)[4], int j) {
+  const uint32_t w = j < 32 ? mw[0] : (j < 64 ? mw[1] : (j < 96 ? mw[2] : mw[3]));
+  return (w >> (j & 31)) & 1u;
+}
+
+// WAIT coin flip of PPOAgent.act (ppo.py:154-156) -> column index to forbid, or -1
+__device__ __forceinline__ int coin_flip(const HeadArgs &a, int64_t row, const uint32_t (&mw)[4]) {
+  if (!(a.wait_ratio >= 0.f) || !a.bits) return -1;
+  int cnt = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) cnt += __popc(mw[w]);
+  const int P = a.wait_index;
+  const bool wait_bad = bit_of(mw, P);
+  if (cnt > 1 && !wait_bad &&
+      uniform_at(a.seed ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio)
+    return P;
+  return -1;
+}
+
+struct RowStats {
+  float m, S, lse, H;
+};
+// Pass 1 writes the masked row back into the tile (-1e7 at invalid entries,
+// ppo.py:119) and finds the max; pass 2 sums p = exp(x - m) and p*x.
+__device__ __forceinline__ RowStats quad_row_stats(float *row, const uint32_t (&mw)[4], int A,
+                                                   int c, int fw) {
+  float m = -INFINITY;
+  for (int j = c; j < A; j += 4) {
+    float x = row[j];
+    if (bit_of(mw, j) || j == fw) {
+      x = kMaskedLogit;
+      row[j] = x;
+    }
+    m = fmaxf(m, x);
+  }
+  m = qmax(m);
+  float S = 0.f, T = 0.f;
+  for (int j = c; j < A; j += 4) {
+    const float x = row[j];
+    const float p = __expf(x - m);
+    S += p;
+    T += p * x;
+  }
+  S = qsum(S);
+  T = qsum(T);
+  RowStats r;
+  r.m = m;
+  r.S = S;
+  r.lse = m + logf(S);
+  r.H = r.lse - T / S;
+  return r;
+}
+
+template <int ROWS>
+__device__ __forceinline__ void tile_rows(int64_t &r0, int &nr) {
+  const int64_t rows = r0;  // caller passes total rows in r0
+  r0 = (int64_t)blockIdx.x * ROWS;
+  nr = (int)min((int64_t)ROWS, rows - r0);
+}
+
+// Forward over a tile of 64 rows (256 threads): per-row logprob / entropy to
+// a.row_lp / a.row_ent; SAMPLE draws by inverse CDF in lane-major order.
+__global__ __launch_bounds__(256) void k_head_fwd_tile(HeadArgs a) {
+  extern __shared__ __align__(16) float tl[];
+  int64_t r0 = (int64_t)a.B * a.V;
+  int nr;
+  tile_rows<64>(r0, nr);
+  tile_load(a.logits + r0 * a.A, tl, nr * a.A);
+  __syncthreads();
+  const int lr = threadIdx.x >> 2, c = threadIdx.x & 3;
+  if (lr >= nr) return;  // whole quads leave together
+  const int64_t row = r0 + lr;
+  float *rp = tl + lr * a.A;
+  if (a.mode == VMP_HEAD_ARGMAX) {  // get_det_action: unmasked, first max
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int j = c; j < a.A; j += 4) {
+      const float x = rp[j];
+      if (x == x && (x > best || bi == 0x7fffffff)) {
+        best = x;
+        bi = j;
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) {
+      const float ob = __shfl_xor(best, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (c == 0) a.action[row] = bi == 0x7fffffff ? 0 : bi;
+    return;
+  }
+  uint32_t mw[4];
+  load_mask_words(a, row, mw);
+  const int fw = coin_flip(a, row, mw);
+  const RowStats st = quad_row_stats(rp, mw, a.A, c, fw);
+  int act;
+  if (a.mode == VMP_HEAD_SAMPLE) {
+    float t = 0.f;
+    for (int j = c; j < a.A; j += 4) t += __expf(rp[j] - st.m);
+    float incl = t + __shfl_up(t, 1, 4) * (c >= 1);
+    incl += __shfl_up(incl, 2, 4) * (c >= 2);
+    const float excl = incl - t;  // per-lane range [excl, incl) of the quad total
+    const float total = __shfl(incl, 3, 4);
+    const float target = uniform_at(a.seed, a.offset + (uint64_t)row) * total;
+    int pick = -1, last = -1;
+    float cum = excl;
+    for (int j = c; j < a.A; j += 4) {
+      const float p = __expf(rp[j] - st.m);
+      if (p > 0.f) {
+        cum += p;
+        last = j;
+        if (pick < 0 && target >= excl && target < cum) pick = j;
+      }
+    }
+    if (pick < 0 && last >= 0 && target >= excl && target < incl) pick = last;
+    // lane-major order: the last lane of the quad whose range starts <= target
+    int any = pick;
+#pragma unroll
+    for (int o = 1; o < 4; o <<= 1) any = max(any, __shfl_xor(any, o));
+    if (any < 0) {  // target past the rounded total: last positive entry
+      int lk = last >= 0 ? c * 1024 + last : -1;
+#pragma unroll
+      for (int o = 1; o < 4; o <<= 1) lk = max(lk, __shfl_xor(lk, o));
+      any = lk & 1023;
+    } else {  // more than one lane can claim only through rounding: lowest lane wins
+      int mine = pick >= 0 ? c : 4;
+#pragma unroll
+      for (int o = 1; o < 4; o <<= 1) mine = min(mine, __shfl_xor(mine, o));
+      any = __shfl(pick, mine, 4);
+    }
+    act = any;
+    if (c == 0) a.action[row] = act;
+  } else {
+    act = a.action[row];
+  }
+  if (c == 0) {
+    const float lp = (act >= 0 && act < a.A) ? rp[act] - st.lse : NAN;
+    a.row_lp[row] = lp;
+    a.row_ent[row] = st.H;
+  }
+}
+
+// Backward over a tile: d/dz_j of (g_lp * logprob + g_ent * entropy)
+//   = -q_j (g_lp + g_ent (x_j - lse + H)) + g_lp [j = a],  0 at masked j,
+// written into the tile in place and streamed out with 16-B stores.
+__global__ __launch_bounds__(256) void k_head_bwd_tile(HeadArgs a) {
+  extern __shared__ __align__(16) float tl[];
+  int64_t r0 = (int64_t)a.B * a.V;
+  int nr;
+  tile_rows<64>(r0, nr);
+  tile_load(a.logits + r0 * a.A, tl, nr * a.A);
+  __syncthreads();
+  const int lr = threadIdx.x >> 2, c = threadIdx.x & 3;
+  if (lr < nr) {
+    const int64_t row = r0 + lr;
+    float *rp = tl + lr * a.A;
+    uint32_t mw[4];
+    load_mask_words(a, row, mw);
+    const RowStats st = quad_row_stats(rp, mw, a.A, c, -1);
+    const int b = (int)(row / a.V);
+    const float glp = a.g_logprob ? a.g_logprob[b] : 0.f;
+    const float gen = a.g_entropy ? a.g_entropy[b] : 0.f;
+    const int act = a.action[row];
+    const float inv = 1.0f / st.S;
+    const float c1 = glp + gen * (st.H - st.lse);
+    for (int j = c; j < a.A; j += 4) {
+      const float x = rp[j];
+      const float q = __expf(x - st.m) * inv;
+      float g = -q * fmaf(gen, x, c1);
+      if (j == act) g += glp;
+      rp[j] = bit_of(mw, j) ? 0.f : g;
+    }
+  }
+  __syncthreads();
+  tile_store(a.dlogits + r0 * a.A, tl, nr * a.A);
+}
+
+// Per-sample sums of the row results (ppo.py:124-125), fixed order: one wave per sample.
+__global__ __launch_bounds__(256) void k_rowsum(int B, int V, const float *row_lp,
+                                                const float *row_ent, float *lp, float *ent) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float s0 = 0.f, s1 = 0.f;
+  for (int v = lane; v < V; v += 64) {
+    s0 += row_lp[(int64_t)b * V + v];
+    s1 += row_ent[(int64_t)b * V + v];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o);
+    s1 += __shfl_xor(s1, o);
+  }
+  if (lane == 0) {
+    if (lp) lp[b] = s0;
+    if (ent) ent[b] = s1;
+  }
+}
+
 // PPOAgent.update GAE (ppo.py:232-243): one lane per env column, reverse scan
 // over T; f32 as the reference's rewards_batch / values.
 __global__ void k_gae(int T, int N, const float *r, const float *d, const float *v,
@@ -332,12 +591,51 @@ int block_threads(int V, int G) {
   VMP_HEAD_CASE(KERN, 16, 4) VMP_HEAD_CASE(KERN, 16, 8) VMP_HEAD_CASE(KERN, 16, 16)      \
   VMP_HEAD_CASE(KERN, 64, 4) VMP_HEAD_CASE(KERN, 64, 8) VMP_HEAD_CASE(KERN, 64, 16)
 
-hipError_t launch_fwd(const HeadArgs &a, hipStream_t st) {
+bool use_tiles(const HeadArgs &a) {
+  return a.A <= kTileMaxA && ((uintptr_t)a.logits & 15) == 0 &&
+         (!a.dlogits || ((uintptr_t)a.dlogits & 15) == 0);
+}
+
+hipError_t launch_fwd(const HeadArgs &a0, hipStream_t st) {
+  if (use_tiles(a0)) {
+    HeadArgs a = a0;
+    const int64_t rows = (int64_t)a.B * a.V;
+    const unsigned grid = (unsigned)((rows + 63) / 64);
+    const size_t lds = (size_t)64 * a.A * sizeof(float);
+    const bool need_sums = a.mode != VMP_HEAD_ARGMAX;
+    float *scratch = nullptr;
+    if (need_sums) {
+      hipError_t e = hipMallocAsync((void **)&scratch, 2 * rows * sizeof(float), st);
+      if (e != hipSuccess) return e;
+      a.row_lp = scratch;
+      a.row_ent = scratch + rows;
+    }
+    hipLaunchKernelGGL(k_head_fwd_tile, dim3(grid), dim3(256), lds, st, a);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && need_sums) {
+      hipLaunchKernelGGL(k_rowsum, dim3((a.B + 3) / 4), dim3(256), 0, st, a.B, a.V, a.row_lp,
+                         a.row_ent, a.logprob, a.entropy);
+      e = hipGetLastError();
+    }
+    if (scratch) {
+      hipError_t f = hipFreeAsync(scratch, st);
+      if (e == hipSuccess) e = f;
+    }
+    return e;
+  }
+  const HeadArgs &a = a0;
   const int G = pick_g(a.A), E = pick_e(a.A, G);
   VMP_HEAD_ALL(k_head_fwd)
   return hipErrorInvalidValue;
 }
 hipError_t launch_bwd(const HeadArgs &a, hipStream_t st) {
+  if (use_tiles(a)) {
+    const int64_t rows = (int64_t)a.B * a.V;
+    const unsigned grid = (unsigned)((rows + 63) / 64);
+    const size_t lds = (size_t)64 * a.A * sizeof(float);
+    hipLaunchKernelGGL(k_head_bwd_tile, dim3(grid), dim3(256), lds, st, a);
+    return hipGetLastError();
+  }
   const int G = pick_g(a.A), E = pick_e(a.A, G);
   VMP_HEAD_ALL(k_head_bwd)
   return hipErrorInvalidValue;
