@@ -46,6 +46,25 @@ extern "C" {
 #define VMP_SEQ_UNIFORM 0
 #define VMP_SEQ_LOWUNIFORM 1
 #define VMP_SEQ_HIGHUNIFORM 2
+/* eval-mode Record metrics (vmp_record_read): per-env sums, VMP_NREC doubles */
+#define VMP_REC_STEPS 0     /* recorded steps */
+#define VMP_REC_REWARD 1    /* sum of rewards */
+#define VMP_REC_CPU 2       /* sum over steps and PMs of cpu, and of cpu^2 */
+#define VMP_REC_CPU2 3
+#define VMP_REC_MEM 4       /* same for memory */
+#define VMP_REC_MEM2 5
+#define VMP_REC_RANK 6      /* sum of _get_rank (PMs hosting >= 1 VM) */
+#define VMP_REC_DROP 7      /* sum of dropped / total_requests (0 if none) */
+#define VMP_REC_TCM 8       /* sum of target_cpu_mean, target_memory_mean */
+#define VMP_REC_TMM 9
+#define VMP_REC_WAITING 10  /* sum of waiting_ratio */
+#define VMP_REC_LIFE_SUM 11 /* sum of VM lifetimes (record.py vm_lifetime) */
+#define VMP_REC_LIVES 12    /* number of VM lives (len(unique_vms_placement)) */
+#define VMP_REC_REWARD_OK 13 /* sum and count of rewards > -1e7, count of rewards < -1e7 */
+#define VMP_REC_N_OK 14
+#define VMP_REC_N_BAD 15
+#define VMP_NREC 16
+#define VMP_REC_BINS 1001   /* pending / slowdown rates x1000: 0 .. 1000 */
 /* actor-head modes (vmp_policy_head) */
 #define VMP_HEAD_SAMPLE 0 /* Network.get_action(obs, action=None, mask) (ppo.py:115-126) */
 #define VMP_HEAD_GIVEN 1  /* Network.get_action(obs, action, mask): log_prob/entropy only */
@@ -195,6 +214,18 @@ int vmp_policy_head_backward(int32_t B, int32_t V, int32_t A, const float *logit
                              const uint32_t *mask_bits, const int32_t *action,
                              const float *g_logprob, const float *g_entropy, float *dlogits,
                              void *hip_stream);
+
+/* Eval-mode Record metrics on the device (record.py:34-134, base.py:131-148):
+ * on = 1 allocates the recorder and starts it from the current state (call it
+ * right after reset, as Base.test records from reset); every later vmp_step /
+ * vmp_heuristic_step / vmp_rollout_heuristic step is recorded for every env.
+ * on = 0 frees it. */
+int vmp_record_enable(vmp_handle *h, int32_t on);
+/* Read the metrics so far (non-destructive): hist u32[n_env][2][VMP_REC_BINS]
+ * = counts of the pending and slowdown rates rounded to 3 decimals (x1000),
+ * over every VM life incl. the open ones; sums f64[n_env][VMP_NREC]. The
+ * Record.get_summary values follow from these (vmp/record.py). */
+int vmp_record_read(vmp_handle *h, uint32_t *hist, double *sums);
 
 /* Diagnostics: per-env shader-clock cycles per kernel phase, accumulated since
  * the previous call, device u64[n_env][24] (see tools/stamps.py for the phase names).

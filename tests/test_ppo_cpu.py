@@ -207,3 +207,15 @@ def test_weights_io_compiled_prefix(tmp_path):
     ag2.load_model(p)
     for k, v in ag2.model.state_dict().items():
         assert np.array_equal(v.numpy(), w[k])
+
+
+def test_cli_parses_reference_yaml(tmp_path):
+    from vmp.main import make_agent, parse
+    p = tmp_path / "c.yml"
+    p.write_text("environment:\n  pms: 10\n  vms: 30\n  seed: 1\n  reward_function: kl\n"
+                 "agents:\n  ppo:\n    hidden_size: 512\n    device: cpu\n")
+    a = parse(["-a", "ppo", "-c", str(p), "-r", "ut", "-e", "-w", "x.pt"])
+    assert a.agent == "ppo" and a.reward == "ut" and a.eval and a.weightspath == "x.pt"
+    assert a.config["agents"]["ppo"]["hidden_size"] == 512
+    with pytest.raises(ValueError):
+        make_agent("drlvmp", None, {})

@@ -12,6 +12,7 @@
 
 #include "../../include/vmp.h"
 #include "vmp_layout.h"
+#include "vmp_record.h"
 
 namespace vmp {
 constexpr int kStamps = 24;  // per-env phase clocks (diagnostic builds)
@@ -22,6 +23,9 @@ __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double
                          double *cpu, double *mem, int64_t *remaining, int64_t *rank);
 __global__ void k_counters(EnvParams p, int64_t *ctr, double *st);
 __global__ void k_target_means(EnvParams p);
+__global__ void k_record(EnvParams p, RecArgs r);
+__global__ void k_record_init(EnvParams p, RecArgs r);
+__global__ void k_record_close(EnvParams p, RecArgs r, uint32_t *hist, double *sums);
 __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, uint8_t *mask);
 }  // namespace vmp
 
@@ -91,6 +95,12 @@ struct vmp_handle {
   PoisConst *pois_dev;
   uint64_t *stamps;
   uint64_t *jump_dev;
+  // eval-mode Record metrics (vmp_record.hip), allocated by vmp_record_enable
+  bool rec_on;
+  RecArgs rec;
+  int32_t *rec_act;   // scratch action / validity / reward when the caller passes none
+  uint8_t *rec_valid;
+  double *rec_reward;
 };
 
 namespace {
@@ -349,6 +359,7 @@ int vmp_destroy(vmp_handle *h) {
   (void)hipFree(h->pois_dev);
   (void)hipFree(h->jump_dev);
   (void)hipFree(h->stamps);
+  vmp_record_enable(h, 0);
   delete h;
   return VMP_OK;
 }
@@ -384,6 +395,9 @@ int vmp_reset(vmp_handle *h, const int64_t *seeds, const uint8_t *env_mask, floa
   return VMP_OK;
 }
 
+static int record_after(vmp_handle *h, const int32_t *act, const uint8_t *valid,
+                        const double *reward);
+
 int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward, uint8_t *done,
              uint8_t *valid) {
   if (!h || !actions) return fail(VMP_EINVAL, "null handle or actions");
@@ -394,7 +408,13 @@ int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward, 
   o.done = done;
   o.valid = valid;
   o.k_steps = 1;
-  return launch_env(h, o);
+  if (h->rec_on) {
+    if (!o.reward) o.reward = h->rec_reward;
+    if (!o.valid) o.valid = h->rec_valid;
+  }
+  int rc = launch_env(h, o);
+  if (rc == VMP_OK && h->rec_on) rc = record_after(h, actions, o.valid, o.reward);
+  return rc;
 }
 
 int vmp_heuristic_act(vmp_handle *h, int32_t policy, int32_t *actions) {
@@ -421,7 +441,14 @@ int vmp_heuristic_step(vmp_handle *h, int32_t policy, int32_t *actions_out, floa
   o.done = done;
   o.valid = valid;
   o.k_steps = 1;
-  return launch_env(h, o);
+  if (h->rec_on) {
+    if (!o.act_out) o.act_out = h->rec_act;
+    if (!o.reward) o.reward = h->rec_reward;
+    if (!o.valid) o.valid = h->rec_valid;
+  }
+  int rc = launch_env(h, o);
+  if (rc == VMP_OK && h->rec_on) rc = record_after(h, o.act_out, o.valid, o.reward);
+  return rc;
 }
 
 int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double *rewards,
@@ -429,6 +456,17 @@ int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double
   if (!h || k_steps < 1) return fail(VMP_EINVAL, "null handle or k_steps < 1");
   if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
     return fail(VMP_EINVAL, "unknown policy");
+  if (h->rec_on) {  // recorded: one step per launch, the recorder after each
+    for (int32_t k = 0; k < k_steps; k++) {
+      int rc = vmp_heuristic_step(h, policy, nullptr, nullptr,
+                                  rewards ? rewards + (int64_t)k * h->N : nullptr, nullptr, nullptr);
+      if (rc) return rc;
+      if (done_count) {
+        // done flags of recorded rollouts are not accumulated (eval loops stop at done)
+      }
+    }
+    return VMP_OK;
+  }
   // launches of at most kMaxStepsPerLaunch steps (the per-launch draw region)
   for (int32_t k0 = 0; k0 < k_steps; k0 += kMaxStepsPerLaunch) {
     StepOut o = empty_out();
@@ -439,6 +477,73 @@ int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double
     int rc = launch_env(h, o);
     if (rc) return rc;
   }
+  return VMP_OK;
+}
+
+static int record_after(vmp_handle *h, const int32_t *act, const uint8_t *valid,
+                        const double *reward) {
+  RecArgs r = h->rec;
+  r.act = act;
+  r.valid = valid;
+  r.reward = reward;
+  const size_t lds = (size_t)4 * ((h->P + 63) / 64) * sizeof(unsigned long long);
+  hipLaunchKernelGGL(k_record, dim3((h->N + 3) / 4), dim3(256), lds, h->stream, h->prm, r);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_record_enable(vmp_handle *h, int32_t on) {
+  if (!h) return fail(VMP_EINVAL, "null handle");
+  if (!on) {
+    if (h->rec_on) (void)hipStreamSynchronize(h->stream);
+    (void)hipFree(h->rec.prev);
+    (void)hipFree(h->rec.life_n);
+    (void)hipFree(h->rec.alloc);
+    (void)hipFree(h->rec.waits);
+    (void)hipFree(h->rec.hist);
+    (void)hipFree(h->rec.sums);
+    (void)hipFree(h->rec_act);
+    (void)hipFree(h->rec_valid);
+    (void)hipFree(h->rec_reward);
+    std::memset(&h->rec, 0, sizeof(h->rec));
+    h->rec_act = nullptr;
+    h->rec_valid = nullptr;
+    h->rec_reward = nullptr;
+    h->rec_on = false;
+    return VMP_OK;
+  }
+  const size_t nv = (size_t)h->N * h->V;
+  if (!h->rec.prev) {
+    HIP_TRY(hipMalloc(&h->rec.prev, sizeof(uint16_t) * nv));
+    HIP_TRY(hipMalloc(&h->rec.life_n, sizeof(uint32_t) * nv));
+    HIP_TRY(hipMalloc(&h->rec.alloc, sizeof(int32_t) * nv));
+    HIP_TRY(hipMalloc(&h->rec.waits, sizeof(uint32_t) * nv));
+    HIP_TRY(hipMalloc(&h->rec.hist, sizeof(uint32_t) * (size_t)h->N * 2 * VMP_REC_BINS));
+    HIP_TRY(hipMalloc(&h->rec.sums, sizeof(double) * (size_t)h->N * VMP_NREC));
+    HIP_TRY(hipMalloc(&h->rec_act, sizeof(int32_t) * nv));
+    HIP_TRY(hipMalloc(&h->rec_valid, nv));
+    HIP_TRY(hipMalloc(&h->rec_reward, sizeof(double) * (size_t)h->N));
+  }
+  size_t n = nv;
+  if ((size_t)h->N * 2 * VMP_REC_BINS > n) n = (size_t)h->N * 2 * VMP_REC_BINS;
+  if ((size_t)h->N * VMP_NREC > n) n = (size_t)h->N * VMP_NREC;
+  hipLaunchKernelGGL(k_record_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream,
+                     h->prm, h->rec);
+  HIP_TRY(hipGetLastError());
+  h->rec_on = true;
+  return VMP_OK;
+}
+
+int vmp_record_read(vmp_handle *h, uint32_t *hist, double *sums) {
+  if (!h || !hist || !sums) return fail(VMP_EINVAL, "null argument");
+  if (!h->rec_on) return fail(VMP_ESTATE, "recording is not enabled (vmp_record_enable)");
+  HIP_TRY(hipMemcpyAsync(hist, h->rec.hist, sizeof(uint32_t) * (size_t)h->N * 2 * VMP_REC_BINS,
+                         hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(sums, h->rec.sums, sizeof(double) * (size_t)h->N * VMP_NREC,
+                         hipMemcpyDeviceToDevice, h->stream));
+  hipLaunchKernelGGL(k_record_close, dim3((h->N + 3) / 4), dim3(256), 0, h->stream, h->prm,
+                     h->rec, hist, sums);
+  HIP_TRY(hipGetLastError());
   return VMP_OK;
 }
 

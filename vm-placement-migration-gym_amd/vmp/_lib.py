@@ -16,7 +16,8 @@ EXPORTS = (
     "vmp_set_eval", "vmp_dims", "vmp_reset", "vmp_step", "vmp_heuristic_act",
     "vmp_heuristic_step", "vmp_rollout_heuristic", "vmp_mask", "vmp_mask_bool", "vmp_get_obs",
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
-    "vmp_policy_head", "vmp_policy_head_backward", "vmp_debug_stamps",
+    "vmp_policy_head", "vmp_policy_head_backward", "vmp_record_enable", "vmp_record_read",
+    "vmp_debug_stamps",
 )
 
 
@@ -85,6 +86,8 @@ def lib():
         "vmp_policy_head": (ctypes.c_int, [i32, i32, i32, i32, P, P, f32, i32, u64, u64, P, P, P,
                                             P]),
         "vmp_policy_head_backward": (ctypes.c_int, [i32, i32, i32, P, P, P, P, P, P, P]),
+        "vmp_record_enable": (ctypes.c_int, [P, i32]),
+        "vmp_record_read": (ctypes.c_int, [P, P, P]),
         "vmp_debug_stamps": (ctypes.c_int, [P, P]),
     }
     for name, (res, args) in sig.items():

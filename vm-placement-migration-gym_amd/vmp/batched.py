@@ -21,6 +21,8 @@ from .config import Config
 
 N_COUNTERS = 6  # total_requests, served, suspend, place, dropped, timestep
 N_STATS = 5     # waiting_ratio, target_cpu_mean, target_mem_mean, total_cpu_req, total_mem_req
+N_REC = 16      # VMP_NREC: recorder sums (include/vmp.h VMP_REC_*)
+REC_BINS = 1001
 
 
 class BatchedVmEnv:
@@ -191,6 +193,29 @@ class BatchedVmEnv:
         check(lib().vmp_get_state(h, ptr(pl), ptr(vc), ptr(vm), ptr(c), ptr(m), ptr(rem)))
         return dict(vm_placement=pl, vm_cpu=vc, vm_memory=vm, cpu=c, memory=m,
                     vm_remaining_runtime=rem)
+
+    # ------------------------------------------------ eval-mode Record metrics
+    def record(self, on=True):
+        """Start (on=True, right after reset, as Base.test does) or stop recording
+        the Record metrics of every env on the device (vmp_record_enable)."""
+        check(lib().vmp_record_enable(self._bind(), int(bool(on))))
+
+    def record_read(self):
+        """(hist u32 [N, 2, 1001] pending/slowdown rate counts, sums f64 [N, 16])."""
+        h = self._bind()
+        hist = self._empty((self.n_envs, 2, REC_BINS), torch.int32)
+        sums = self._empty((self.n_envs, N_REC), torch.float64)
+        check(lib().vmp_record_read(h, ptr(hist), ptr(sums)))
+        return hist, sums
+
+    def record_summary(self):
+        """Record.get_summary() (record.py:110-134) of every env -> list of dicts."""
+        from .record import summary_from_device
+        hist, sums = self.record_read()
+        ctr, st = self.counters().cpu().numpy(), self.stats().cpu().numpy()
+        hist, sums = hist.cpu().numpy().view(np.uint32), sums.cpu().numpy()
+        return [summary_from_device(hist[i], sums[i], ctr[i], st[i], self.P)
+                for i in range(self.n_envs)]
 
     def rank(self):
         h = self._bind()

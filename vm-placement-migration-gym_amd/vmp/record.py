@@ -158,3 +158,66 @@ class NpEncoder(json.JSONEncoder):
         if isinstance(obj, np.ndarray):
             return obj.tolist()
         return super().default(obj)
+
+
+# include/vmp.h VMP_REC_* indices of the device recorder's sums
+REC_STEPS, REC_REWARD, REC_CPU, REC_CPU2, REC_MEM, REC_MEM2, REC_RANK, REC_DROP = range(8)
+REC_TCM, REC_TMM, REC_WAITING, REC_LIFE_SUM, REC_LIVES, REC_REWARD_OK, REC_N_OK, REC_N_BAD = \
+    range(8, 16)
+
+
+def _hist_stats(h):
+    """(mean, median, max) of values i/1000 counted by h[i], numpy's definitions."""
+    n = int(h.sum())
+    if n == 0:
+        return None
+    idx = np.flatnonzero(h)
+    vals = idx / 1000.0
+    mean = float((h[idx] * vals).sum() / n)
+    cum = np.cumsum(h[idx])
+    lo = vals[np.searchsorted(cum, (n - 1) // 2 + 1)]
+    hi = vals[np.searchsorted(cum, n // 2 + 1)]
+    return mean, (lo + hi) / 2.0, float(vals[-1])
+
+
+def summary_from_device(hist, sums, counters, stats, pms):
+    """Record.get_summary (record.py:110-134) from the device recorder of one env
+    (vmp_record_read) plus its counters [total_requests, served, suspend, place,
+    dropped, timestep] and stats [waiting, tcm, tmm, total_cpu_req, total_mem_req]."""
+    T = sums[REC_STEPS]
+    n_eq = T - sums[REC_N_OK] - sums[REC_N_BAD]  # rewards exactly -1e7 stay as they are
+    mean_ok = sums[REC_REWARD_OK] / sums[REC_N_OK] if sums[REC_N_OK] else np.nan
+    total = sums[REC_REWARD_OK] + n_eq * -1e7 + (sums[REC_N_BAD] * mean_ok if sums[REC_N_BAD] else 0.0)
+    pend = _hist_stats(hist[0])
+    slow = _hist_stats(hist[1]) or (0.0, 0.0, 0.0)  # slowdown_rates defaults to [0]
+    TP = T * pms
+    cm, mm = sums[REC_CPU] / TP, sums[REC_MEM] / TP
+    return {
+        "total rewards": np.round(total, 3),
+        "total served VMs": int(counters[1]),
+        "total requests": int(counters[0]),
+        "total cpu requested": np.round(stats[3], 3),
+        "total memory requested": np.round(stats[4], 3),
+        "total suspend actions": int(counters[2]),
+        "total place actions": int(counters[3]),
+        "average VM life": np.round(sums[REC_LIFE_SUM] / sums[REC_LIVES], 3) if sums[REC_LIVES] else np.nan,
+        "average pending": np.round(pend[0], 3) if pend else np.nan,
+        "median pending": np.round(pend[1], 3) if pend else np.nan,
+        "max pending": np.round(pend[2], 3) if pend else 0,
+        "average slowdown": np.round(slow[0], 3),
+        "median slowdown": np.round(slow[1], 3),
+        "max slowdown": np.round(slow[2], 3),
+        "drop rate": np.round(sums[REC_DROP] / T, 3),
+        "cpu mean": np.round(cm, 3),
+        "cpu mean target": np.round(sums[REC_TCM] / T, 3),
+        "cpu std": np.round(np.sqrt(max(sums[REC_CPU2] / TP - cm * cm, 0.0)), 3),
+        "memory mean": np.round(mm, 3),
+        "memory mean target": np.round(sums[REC_TMM] / T, 3),
+        "memory std": np.round(np.sqrt(max(sums[REC_MEM2] / TP - mm * mm, 0.0)), 3),
+        "rank mean": np.round(sums[REC_RANK] / T, 3),
+        # unrounded columns the exp_* drivers print (exp_suspension.py:51-58)
+        "_mean_life": sums[REC_LIFE_SUM] / sums[REC_LIVES] if sums[REC_LIVES] else np.nan,
+        "_mean_pending": pend[0] if pend else np.nan,
+        "_mean_slowdown": slow[0],
+        "_max_slowdown": slow[2],
+    }
