@@ -204,13 +204,13 @@ void launch_vpt(int need, dim3 grid, dim3 block, size_t lds, hipStream_t s, cons
 }
 
 int launch_env(vmp_handle *h, const StepOut &o) {
-  dim3 grid((h->N + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
+  dim3 grid((h->N + kEnvWavesPerBlock - 1) / kEnvWavesPerBlock), block(64 * kEnvWavesPerBlock);
   EnvParams p = h->prm;
   // per-launch region: speculative service draws (state + value) and arrivals
   p.scap = kSpecDraws;
   const int64_t pre = 20 * (int64_t)p.scap + 4 * (int64_t)(o.k_steps > 0 ? o.k_steps : 1);
   p.lds_wave_bytes = (int32_t)align16(p.off_pre + pre);
-  size_t lds = (size_t)p.lds_wave_bytes * kWavesPerBlock;
+  size_t lds = (size_t)p.lds_wave_bytes * kEnvWavesPerBlock;
   if (lds > 160 * 1024 - 2048) return fail(VMP_EINVAL, "config too large for the LDS carve");
   const int need = (h->V + 63) / 64;
   if (o.k_steps == 1) launch_vpt<true>(need, grid, block, lds, h->stream, p, o);

@@ -1442,7 +1442,7 @@ __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, con
 // ONE = true is the per-step launch (k_steps == 1, the Base.test loop body); it
 // is a separate instantiation so profiles tell it apart from fused rollouts.
 template <int VPT, bool ONE>
-__global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
+__global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
   extern __shared__ __align__(16) char lds[];
   __shared__ Tables T;
 #ifdef VMP_STAMPS
@@ -1451,7 +1451,7 @@ __global__ __launch_bounds__(256, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU)
 #endif
   const int lane = lane_id();
   const int wid = threadIdx.x >> 6;
-  const int e_raw = uni(blockIdx.x * kWavesPerBlock + wid);
+  const int e_raw = uni(blockIdx.x * kEnvWavesPerBlock + wid);
   const int e = e_raw < p.N ? e_raw : p.N - 1;  // tail waves load a valid env, then leave
   char LDSP *base = (char LDSP *)lds + wid * p.lds_wave_bytes;
   const Lds L = make_lds(p, base);

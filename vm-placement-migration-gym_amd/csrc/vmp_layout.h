@@ -23,6 +23,11 @@ namespace vmp {
 
 constexpr int kWaveSize = 64;
 constexpr int kWavesPerBlock = 4;
+// envs (waves) per workgroup of the env kernel k_env
+#ifndef VMP_ENV_WPB
+#define VMP_ENV_WPB 1
+#endif
+constexpr int kEnvWavesPerBlock = VMP_ENV_WPB;
 constexpr int kMaxVPT = 16;  // VM slots per lane held in registers: V <= 1024
 constexpr int kMaxStepsPerLaunch = 256;  // rollout launches are split by the host
 constexpr int kSpecDraws = 64;           // speculative service draws per launch
