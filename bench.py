@@ -303,25 +303,17 @@ def bench_ppo_eval(args, dev, rank, world, dist):
     w = np.load(os.path.join(ROOT, "tests", "golden", "ppo10_wr_weights.npz"))
     ag.model.load_state_dict({k: torch.tensor(w[k]) for k in w.files})
     ag.eval(True)
-    obs = env.obs()
-    bits = torch.empty((N, env.V, env.W), dtype=torch.int32, device=dev)
-    rew = torch.empty((N,), dtype=torch.float64, device=dev)
-    done = torch.empty((N,), dtype=torch.uint8, device=dev)
-
-    def step():
-        env.mask_bits(out=bits)
-        a = ag.act_batch(obs, bits)
-        env.step(a, obs=obs, reward=rew, done=done, want_valid=False)
-
+    from vmp.ppo import ActStepGraph
+    g = ActStepGraph(ag)  # mask + actor + head + step captured once, replayed per step
     for _ in range(10):
-        step()
+        g.replay()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     K = 200
     t0 = time.perf_counter()
     for _ in range(K):
-        step()
+        g.replay()
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -329,7 +321,8 @@ def bench_ppo_eval(args, dev, rank, world, dist):
     env.close()
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f32",
             "workload": "config/10.yml (P10 V30), PPO eval, weights-10/ppo-wr.pt, masked, "
-                        "migration_ratio 0.5", "envs_per_gpu": N, "steps": K,
+                        "migration_ratio 0.5, one HIP graph per batched step",
+            "envs_per_gpu": N, "steps": K,
             "ms_per_step": 1e3 * el / K}
 
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 2
+#define VMP_ABI_VERSION 3
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -194,6 +194,10 @@ int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const 
  *    both nullable.
  *  - VMP_HEAD_ARGMAX: get_det_action (ppo.py:128-131), argmax of the unmasked
  *    row, first index on ties; logprob/entropy untouched.
+ *  - rng_counter (nullable): a device u64 whose current value is mixed into the
+ *    seed, so a captured graph that advances it between replays draws fresh
+ *    actions; workspace (nullable): 2*B*V floats of row scratch (else the call
+ *    allocates stream-ordered memory, which graph capture may not support).
  *  - wait_ratio >= 0 applies PPOAgent.act's WAIT coin flips first (ppo.py:154-156):
  *    a row with > 1 invalid entries whose column wait_index (= P) is valid
  *    gets it forbidden when a uniform draw exceeds wait_ratio
@@ -202,8 +206,8 @@ int vmp_gae(int32_t T, int32_t N, const float *reward, const float *done, const 
  * All pointers are device pointers; A <= VMP_HEAD_MAX_A. */
 int vmp_policy_head(int32_t B, int32_t V, int32_t A, int32_t mode, const float *logits,
                     const uint32_t *mask_bits, float wait_ratio, int32_t wait_index,
-                    uint64_t seed, uint64_t offset, int32_t *action, float *logprob,
-                    float *entropy, void *hip_stream);
+                    uint64_t seed, uint64_t offset, const uint64_t *rng_counter, int32_t *action,
+                    float *logprob, float *entropy, float *workspace, void *hip_stream);
 
 /* Backward of vmp_policy_head (VMP_HEAD_SAMPLE/GIVEN, no coin flips) for the
  * PPO loss (ppo.py:258-277): given dL/dlogprob[B] and dL/dentropy[B]

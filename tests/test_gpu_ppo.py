@@ -209,3 +209,43 @@ def test_batched_rollout_and_update():
     tr.collect()  # continues from last_obs across the episode boundary
     assert torch.isfinite(tr.logp).all()
     env.close()
+
+
+def test_act_step_graph_equals_eager():
+    """ActStepGraph (mask + actor + head + step as one HIP graph) replays the
+    same computation as the eager calls with the counter-mode sampling stream:
+    identical env state, rewards and obs after 30 steps; replays draw fresh
+    actions (the counter advances)."""
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import ActStepGraph, PPOAgent, PPOConfig
+    cfg = Config(**dict(CFG10, arrival_rate=1.0, service_length=15, eval_steps=1000))
+    outs = []
+    for graphed in (True, False):
+        torch.manual_seed(0)
+        env = BatchedVmEnv(cfg, 256, device=DEV)
+        env.eval(True)
+        ag = PPOAgent(env, PPOConfig(hidden_size=64, masked=True, migration_ratio=0.5))
+        ag.model.rng.seed = 1234
+        ag.eval(True)
+        if graphed:
+            g = ActStepGraph(ag, warmup=0)
+            c0 = int(ag.model.rng.counter)
+            for _ in range(30):
+                obs, rew, done = g.replay()
+            assert int(ag.model.rng.counter) == c0 + 30
+        else:
+            ag.model.rng.graph_counter(env.device)
+            obs = env.obs()
+            bits = torch.empty((256, env.V, env.W), dtype=torch.int32, device=DEV)
+            rew = torch.empty(256, dtype=torch.float64, device=DEV)
+            done = torch.empty(256, dtype=torch.uint8, device=DEV)
+            for _ in range(30):  # capture records without running: 30 replays = 30 steps
+                env.mask_bits(out=bits)
+                a = ag.act_batch(obs, bits)
+                env.step(a, obs=obs, reward=rew, done=done, want_valid=False)
+        st = env.state()
+        outs.append((obs.clone(), rew.clone(), st["vm_placement"].clone(), env.counters().clone()))
+        env.close()
+    for x, y in zip(outs[0], outs[1]):
+        assert torch.equal(x, y)

@@ -58,6 +58,7 @@ struct HeadArgs {
   int B, V, A, W, mode, wait_index;
   float wait_ratio;
   uint64_t seed, offset;
+  const uint64_t *ctr;   // nullable device counter mixed into the seed (graph replays)
   const float *logits;
   const uint32_t *bits;
   int32_t *action;       // in (GIVEN) or out (SAMPLE / ARGMAX), [B][V]
@@ -67,6 +68,12 @@ struct HeadArgs {
   float *dlogits;        // backward output [B][V][A] (may alias logits)
   float *row_lp, *row_ent;  // tiled kernels: per-row results [B*V]
 };
+
+// Seed of this launch: with a device counter (captured graphs replay the same
+// arguments) the counter's current value is mixed in.
+__device__ __forceinline__ uint64_t eff_seed(const HeadArgs &a) {
+  return a.ctr ? a.seed ^ mix64(*a.ctr + 0x5851F42D4C957F2Dull) : a.seed;
+}
 
 // Loads one row into registers with the mask applied and, for SAMPLE/GIVEN,
 // the WAIT coin flip of PPOAgent.act (ppo.py:154-156):
@@ -89,7 +96,7 @@ __device__ __forceinline__ void load_row(const HeadArgs &a, int64_t row, int g, 
     int P = a.wait_index;
     bool wait_bad = (mb[P >> 5] >> (P & 31)) & 1u;
     if (cnt > 1 && !wait_bad)
-      forbid_wait = uniform_at(a.seed ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio;
+      forbid_wait = uniform_at(eff_seed(a) ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio;
   }
 #pragma unroll
   for (int e = 0; e < E; e++) {
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(256) void k_head_fwd(HeadArgs a) {
     row_stats<G, E>(x, g, a.A, p, S, lse, H);
     int act;
     if (sample) {
-      act = sample_row<G, E>(p, g, a.A, uniform_at(a.seed, a.offset + (uint64_t)row));
+      act = sample_row<G, E>(p, g, a.A, uniform_at(eff_seed(a), a.offset + (uint64_t)row));
       if (g == 0) a.action[row] = act;
     } else {
       act = a.action[row];
@@ -355,7 +362,7 @@ __device__ __forceinline__ int coin_flip(const HeadArgs &a, int64_t row, const u
   const int P = a.wait_index;
   const bool wait_bad = bit_of(mw, P);
   if (cnt > 1 && !wait_bad &&
-      uniform_at(a.seed ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio)
+      uniform_at(eff_seed(a) ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio)
     return P;
   return -1;
 }
@@ -448,7 +455,7 @@ __global__ __launch_bounds__(256) void k_head_fwd_tile(HeadArgs a) {
     incl += __shfl_up(incl, 2, 4) * (c >= 2);
     const float excl = incl - t;  // per-lane range [excl, incl) of the quad total
     const float total = __shfl(incl, 3, 4);
-    const float target = uniform_at(a.seed, a.offset + (uint64_t)row) * total;
+    const float target = uniform_at(eff_seed(a), a.offset + (uint64_t)row) * total;
     int pick = -1, last = -1;
     float cum = excl;
     for (int j = c; j < a.A; j += 4) {
@@ -605,10 +612,14 @@ hipError_t launch_fwd(const HeadArgs &a0, hipStream_t st) {
     const bool need_sums = a.mode != VMP_HEAD_ARGMAX;
     float *scratch = nullptr;
     if (need_sums) {
-      hipError_t e = hipMallocAsync((void **)&scratch, 2 * rows * sizeof(float), st);
-      if (e != hipSuccess) return e;
-      a.row_lp = scratch;
-      a.row_ent = scratch + rows;
+      float *ws = a.row_lp;  // caller's workspace (2*B*V floats) if given
+      if (!ws) {
+        hipError_t e = hipMallocAsync((void **)&scratch, 2 * rows * sizeof(float), st);
+        if (e != hipSuccess) return e;
+        ws = scratch;
+      }
+      a.row_lp = ws;
+      a.row_ent = ws + rows;
     }
     hipLaunchKernelGGL(k_head_fwd_tile, dim3(grid), dim3(256), lds, st, a);
     hipError_t e = hipGetLastError();
@@ -651,8 +662,8 @@ extern "C" {
 
 int vmp_policy_head(int32_t B, int32_t V, int32_t A, int32_t mode, const float *logits,
                     const uint32_t *mask_bits, float wait_ratio, int32_t wait_index,
-                    uint64_t seed, uint64_t offset, int32_t *action, float *logprob,
-                    float *entropy, void *stream) {
+                    uint64_t seed, uint64_t offset, const uint64_t *rng_counter, int32_t *action,
+                    float *logprob, float *entropy, float *workspace, void *stream) {
   if (B < 0 || V < 1 || A < 1 || A > VMP_HEAD_MAX_A || !logits || !action)
     return vmp::policy_fail(VMP_EINVAL, "vmp_policy_head: bad shape or null pointer");
   if (mode != VMP_HEAD_SAMPLE && mode != VMP_HEAD_GIVEN && mode != VMP_HEAD_ARGMAX)
@@ -662,7 +673,8 @@ int vmp_policy_head(int32_t B, int32_t V, int32_t A, int32_t mode, const float *
   if (B == 0) return VMP_OK;
   HeadArgs a{};
   a.B = B, a.V = V, a.A = A, a.W = (A + 31) / 32, a.mode = mode, a.wait_index = wait_index;
-  a.wait_ratio = wait_ratio, a.seed = seed, a.offset = offset;
+  a.wait_ratio = wait_ratio, a.seed = seed, a.offset = offset, a.ctr = rng_counter;
+  a.row_lp = workspace;
   a.logits = logits, a.bits = mask_bits, a.action = action, a.logprob = logprob,
   a.entropy = entropy;
   hipError_t e = launch_fwd(a, (hipStream_t)stream);

@@ -84,7 +84,7 @@ def lib():
         "vmp_get_rank": (ctypes.c_int, [P, P]),
         "vmp_gae": (ctypes.c_int, [i32, i32, P, P, P, P, f32, f32, P, P, P]),
         "vmp_policy_head": (ctypes.c_int, [i32, i32, i32, i32, P, P, f32, i32, u64, u64, P, P, P,
-                                            P]),
+                                            P, P, P]),
         "vmp_policy_head_backward": (ctypes.c_int, [i32, i32, i32, P, P, P, P, P, P, P]),
         "vmp_record_enable": (ctypes.c_int, [P, i32]),
         "vmp_record_read": (ctypes.c_int, [P, P, P]),
@@ -93,7 +93,7 @@ def lib():
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 2:
+    if L.vmp_abi_version() != 3:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

@@ -53,23 +53,39 @@ def pack_mask(invalid_mask, V, A):
 
 class HeadRng:
     """Counter-based sampling stream: (seed, offset) advanced by B*V per call,
-    so every (sample, VM) draw of a run is distinct and reproducible."""
+    so every (sample, VM) draw of a run is distinct and reproducible.
+    `graph_counter(device)` switches to a device-side counter (one int64
+    tensor, advanced on the stream after each use) for captured graphs, whose
+    replays repeat the launch arguments."""
 
     def __init__(self, seed: int):
         self.seed = int(seed) & (2**64 - 1)
         self.offset = 0
+        self.counter = None
+
+    def graph_counter(self, device):
+        if self.counter is None:
+            self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+        return self
 
     def take(self, n):
+        if self.counter is not None:
+            return self.seed, 0
         o = self.offset
         self.offset += int(n)
         return self.seed, o
+
+    def advance(self):
+        if self.counter is not None:
+            self.counter.add_(1)
 
 
 class MaskedHead(torch.autograd.Function):
     """(logits [B, V*A], bits|None, action|None) -> (action i32 [B,V], logprob [B], entropy [B])."""
 
     @staticmethod
-    def forward(ctx, logits, bits, action, V, A, rng_seed, rng_offset, wait_ratio, wait_index):
+    def forward(ctx, logits, bits, action, V, A, rng_seed, rng_offset, wait_ratio, wait_index,
+                rng_counter=None):
         _need_device(logits, "MaskedHead")
         B = logits.shape[0]
         if logits.dtype != torch.float32:
@@ -87,9 +103,10 @@ class MaskedHead(torch.autograd.Function):
             act = action.to(device=logits.device, dtype=torch.int32).reshape(B, V).contiguous()
         lp = torch.empty((B,), dtype=torch.float32, device=logits.device)
         ent = torch.empty((B,), dtype=torch.float32, device=logits.device)
+        ws = torch.empty((2 * B * V,), dtype=torch.float32, device=logits.device)
         check(lib().vmp_policy_head(B, V, A, mode, ptr(logits), ptr(bits), float(wait_ratio),
-                                    int(wait_index), rng_seed, rng_offset, ptr(act), ptr(lp),
-                                    ptr(ent), _stream(logits)))
+                                    int(wait_index), rng_seed, rng_offset, ptr(rng_counter),
+                                    ptr(act), ptr(lp), ptr(ent), ptr(ws), _stream(logits)))
         ctx.save_for_backward(logits, bits, act)
         ctx.V, ctx.A = V, A
         ctx.mark_non_differentiable(act)
@@ -104,7 +121,7 @@ class MaskedHead(torch.autograd.Function):
         gen = None if g_ent is None else g_ent.float().contiguous()
         check(lib().vmp_policy_head_backward(B, ctx.V, ctx.A, ptr(logits), ptr(bits), ptr(act),
                                              ptr(glp), ptr(gen), ptr(d), _stream(logits)))
-        return d, None, None, None, None, None, None, None, None
+        return d, None, None, None, None, None, None, None, None, None
 
 
 def policy_head(logits, V, A, bits=None, action=None, rng: HeadRng = None, wait_ratio=-1.0,
@@ -117,7 +134,11 @@ def policy_head(logits, V, A, bits=None, action=None, rng: HeadRng = None, wait_
     if wait_ratio >= 0 and torch.is_grad_enabled() and logits.requires_grad:
         raise ValueError("WAIT coin flips (PPOAgent.act) are inference-only")
     seed, off = rng.take(logits.shape[0] * V) if rng is not None else (0, 0)
-    return MaskedHead.apply(logits, bits, action, V, A, seed, off, wait_ratio, wait_index)
+    ctr = rng.counter if rng is not None else None
+    out = MaskedHead.apply(logits, bits, action, V, A, seed, off, wait_ratio, wait_index, ctr)
+    if rng is not None and action is None:
+        rng.advance()
+    return out
 
 
 def det_action(logits, V, A):
@@ -126,8 +147,8 @@ def det_action(logits, V, A):
     logits = logits.float().contiguous()
     B = logits.shape[0]
     act = torch.empty((B, V), dtype=torch.int32, device=logits.device)
-    check(lib().vmp_policy_head(B, V, A, HEAD_ARGMAX, ptr(logits), None, -1.0, -1, 0, 0,
-                                ptr(act), None, None, _stream(logits)))
+    check(lib().vmp_policy_head(B, V, A, HEAD_ARGMAX, ptr(logits), None, -1.0, -1, 0, 0, None,
+                                ptr(act), None, None, None, _stream(logits)))
     return act
 
 

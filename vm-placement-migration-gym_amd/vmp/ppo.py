@@ -126,6 +126,43 @@ class Network(nn.Module):
         return a[0] if obs.dim() == 1 or obs.shape[0] == 1 else a
 
 
+class ActStepGraph:
+    """One batched `PPOAgent.act` + `env.step` for every env (the Base.test loop
+    body, base.py:71-86, with the PPO agent) captured as a HIP graph: mask bits
+    (vmp_mask), actor MLP, masked head with the WAIT coin flips, vmp_step. A
+    replay advances all envs one step with no host work; the head's sampling
+    stream moves through a device counter (HeadRng.graph_counter), so replays
+    draw fresh actions. obs / reward / done are static buffers updated in place."""
+
+    def __init__(self, agent, warmup=2):
+        env = agent.benv
+        dev = env.device
+        self.agent, self.env = agent, env
+        agent.model.rng.graph_counter(dev)
+        self.obs = env.obs()
+        self.bits = torch.empty((env.n_envs, env.V, env.W), dtype=torch.int32, device=dev)
+        self.reward = torch.empty((env.n_envs,), dtype=torch.float64, device=dev)
+        self.done = torch.empty((env.n_envs,), dtype=torch.uint8, device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side), torch.no_grad():
+            for _ in range(warmup):
+                self._step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self._step()
+
+    def _step(self):
+        self.env.mask_bits(out=self.bits)
+        a = self.agent.act_batch(self.obs, self.bits)
+        self.env.step(a, obs=self.obs, reward=self.reward, done=self.done, want_valid=False)
+
+    def replay(self):
+        self.graph.replay()
+        return self.obs, self.reward, self.done
+
+
 def strip_compiled_prefix(sd):
     return {k.replace("_orig_mod.", "", 1) if k.startswith("_orig_mod.") else k: v
             for k, v in sd.items()}
