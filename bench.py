@@ -66,7 +66,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        import datetime
+        # a rank that fails a leg must not leave the others waiting forever
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                timeout=datetime.timedelta(seconds=300))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
