@@ -197,9 +197,10 @@ def main():
         except Exception:
             traffic = None
     env.close()
-    ppo_train = ppo_eval = None
+    ppo_train = ppo_train_bf16 = ppo_eval = None
     if not args.no_ppo:
         ppo_train = _guard(bench_ppo_train, args, dev, rank, world, dist)
+        ppo_train_bf16 = _guard(bench_ppo_train, args, dev, rank, world, dist, "bf16")
         ppo_eval = _guard(bench_ppo_eval, args, dev, rank, world, dist)
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
@@ -219,6 +220,7 @@ def main():
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},
         "parity": parity,
         "ppo_train": ppo_train,
+        "ppo_train_bf16": ppo_train_bf16,
         "ppo_eval": ppo_eval,
     }
     if rank == 0:
@@ -243,7 +245,7 @@ def _max_over_ranks(x, dev, dist):
     return x
 
 
-def bench_ppo_train(args, dev, rank, world, dist):
+def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
     """BASELINE config 3 (config/100.yml, PPO from scratch, reward wr, 8192 envs per
     GPU): one untimed update, then one timed update = batch_size rollout steps of
     every env + PPOAgent.update (4 epochs x 4 minibatches), data-parallel over ranks
@@ -258,7 +260,7 @@ def bench_ppo_train(args, dev, rank, world, dist):
                  sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
     env = BatchedVmEnv(cfg, N, seeds=4 * (rank * N + np.arange(N, dtype=np.int64)), device=dev)
     ag = PPOAgent(env, PPOConfig(hidden_size=512, batch_size=100, minibatch_size=25,
-                                 migration_ratio=0.002, masked=True))
+                                 migration_ratio=0.002, masked=True, precision=precision))
     tr = ag.trainer()
     tr.collect()
     tr.update()
@@ -277,7 +279,8 @@ def bench_ppo_train(args, dev, rank, world, dist):
     total = _max_over_ranks(t2 - t0, dev, dist)
     steps = world * N * tr.T
     env.close()
-    return {"value": steps / total, "unit": "env-steps/s", "dtype": "f32",
+    return {"value": steps / total, "unit": "env-steps/s",
+            "dtype": "f32" if precision == "f32" else "bf16 GEMM inputs, f32 accumulate/params",
             "workload": "config/100.yml (P100 V300), PPO train from scratch, reward wr, "
                         "hidden 512, batch 100 / minibatch 25, 4 epochs",
             "envs_per_gpu": N, "global_envs": world * N, "updates_timed": 1,

@@ -31,9 +31,14 @@ def _need_gpu():
         pytest.fail("gpu tests need a HIP device")
 
 
+@pytest.mark.parametrize("big", [False, True], ids=["wave", "block"])
 @pytest.mark.parametrize("name", T.traj_names())
-def test_trajectory_replay_hip(name):
+def test_trajectory_replay_hip(name, big, monkeypatch):
+    """Every golden trajectory through the wave-per-env kernel (k_env) and the
+    block-per-env kernel of large V (k_env_big, forced with VMP_BIG_KERNEL=1)."""
     from vmp.batched import BatchedVmEnv
+    if big:
+        monkeypatch.setenv("VMP_BIG_KERNEL", "1")
     d = T.load(name)
     envs = []
     for r in d["rewards"]:
@@ -111,13 +116,16 @@ BATCH_CFGS = [
 ]
 
 
+@pytest.mark.parametrize("big", [False, True], ids=["wave", "block"])
 @pytest.mark.parametrize("policy", ["firstfit", "bestfit"])
 @pytest.mark.parametrize("ci", range(len(BATCH_CFGS)))
-def test_batched_heuristic_vs_oracle(ci, policy):
+def test_batched_heuristic_vs_oracle(ci, policy, big, monkeypatch):
     """N envs (seeds base + 4i, incl. > 2**32) stepped by the fused act+step kernel
     against the oracle env by env; then a fused K-step rollout continues and must
-    equal the oracle's next K steps."""
+    equal the oracle's next K steps (both env kernels)."""
     from vmp.batched import BatchedVmEnv
+    if big:
+        monkeypatch.setenv("VMP_BIG_KERNEL", "1")
     base = dict(training_steps=10000, eval_steps=100000, allow_null_action=True, seed=0)
     base.update(BATCH_CFGS[ci])
     N, steps, K = 24, 120, 60
@@ -226,3 +234,50 @@ def test_gae_matches_reference_loop():
     torch.cuda.synchronize()
     assert torch.allclose(adv.cpu(), adv_ref, atol=1e-5, rtol=1e-5)
     assert torch.allclose(ret.cpu(), adv_ref + v, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("policy,reward", [("firstfit", "wr"), ("bestfit", "kl"), (None, "ut")])
+def test_large_v_block_kernel_vs_oracle(policy, reward):
+    """V > 1024 runs k_env_big (one workgroup per env): P1000 / V3000 and
+    P200 / V10000 (the stress config's slot count) against the C oracle,
+    heuristic act+step and random external actions, bit-exact."""
+    from vmp.batched import BatchedVmEnv
+    for P, V, lam, L, steps in ((1000, 3000, 9.0, 300, 40), (200, 10000, 30.0, 400, 25)):
+        cfg = dict(pms=P, vms=V, arrival_rate=lam, service_length=L, training_steps=10000,
+                   eval_steps=100000, seed=5, reward_function=reward, sequence="uniform",
+                   cap_target_util=True, beta=0.5, allow_null_action=True)
+        n = 2
+        seeds = np.array([5, 9], dtype=np.int64)
+        b = BatchedVmEnv(_cfg(cfg), n, seeds=seeds, device=DEV)
+        b.eval(True)
+        orc = [O.OracleEnv(dict(cfg, seed=int(s))) for s in seeds]
+        for e, s in zip(orc, seeds):
+            e.eval(True)
+            e.reset(int(s))
+        g = np.random.default_rng(1)
+        for t in range(steps):
+            if policy is None:
+                st = b.state()["vm_placement"].cpu().numpy()
+                a = st.copy()
+                u = g.random(st.shape)
+                a[(st == P) & (u < 0.3)] = g.integers(0, P, size=int(((st == P) & (u < 0.3)).sum()))
+                a[(st < P) & (u < 0.02)] = P
+                _, rew, _, _ = b.step(torch.tensor(a, dtype=torch.int32, device=DEV))
+                acts = a
+            else:
+                _, rew, _, _, act = b.heuristic_step(policy, want_actions=True)
+                acts = act.cpu().numpy()
+            rew = rew.cpu().numpy()
+            for i, e in enumerate(orc):
+                if policy is not None:
+                    exp = e.firstfit() if policy == "firstfit" else e.bestfit()
+                    assert np.array_equal(exp, acts[i]), (P, V, t, i)
+                _, r, _, _ = e.step(acts[i].astype(np.int64))
+                assert r == rew[i] or abs(r - rew[i]) <= 1e-12 * max(1.0, abs(r)), (P, V, t, i)
+        sd = b.state()
+        for i, e in enumerate(orc):
+            so = e.state()
+            assert np.array_equal(sd["vm_placement"][i].cpu().numpy(), so[0]), (P, V)
+            assert np.array_equal(sd["cpu"][i].cpu().numpy(), so[3]), (P, V)
+            assert np.array_equal(b.counters()[i].cpu().numpy(), e.counters()[0]), (P, V)
+        b.close()

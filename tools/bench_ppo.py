@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--vms", type=int, default=300)
     ap.add_argument("--hidden", type=int, default=512)
     ap.add_argument("--chunk-gb", type=float, default=4.0)
+    ap.add_argument("--precision", default="f32", choices=["f32", "bf16"])
     args = ap.parse_args()
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
@@ -40,7 +41,8 @@ def main():
     env = BatchedVmEnv(cfg, args.envs, device="cuda:0")
     ag = PPOAgent(env, PPOConfig(hidden_size=args.hidden, masked=True, batch_size=100,
                                  minibatch_size=25, migration_ratio=0.002,
-                                 chunk_bytes=int(args.chunk_gb * (1 << 30))))
+                                 chunk_bytes=int(args.chunk_gb * (1 << 30)),
+                                 precision=args.precision))
     tr = ag.trainer()
     for _ in range(args.warmup):
         tr.collect()
@@ -58,7 +60,7 @@ def main():
         tc += t1 - t0
         tu += t2 - t1
     steps = args.envs * tr.T * args.updates
-    out = {"workload": f"PPO train P{args.pms} V{args.vms} hidden {args.hidden}",
+    out = {"workload": f"PPO train P{args.pms} V{args.vms} hidden {args.hidden} {args.precision}",
            "envs": args.envs, "updates": args.updates, "env_steps": steps,
            "value": steps / (tc + tu), "unit": "env-steps/s",
            "collect_s_per_update": tc / args.updates, "update_s_per_update": tu / args.updates,

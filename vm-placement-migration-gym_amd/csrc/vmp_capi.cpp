@@ -18,6 +18,14 @@ namespace vmp {
 constexpr int kStamps = 24;  // per-env phase clocks (diagnostic builds)
 template <int VPT, bool ONE>
 __global__ void k_env(EnvParams p, StepOut o);
+template <int SPT>
+__global__ void k_env_big(EnvParams p, StepOut o);
+extern template __global__ void k_env_big<20>(EnvParams p, StepOut o);
+__global__ void k_rank(EnvParams p, int64_t *rank);
+__global__ void k_target_means_lds(EnvParams p);
+constexpr int kBigMaxThreads = 512;  // k_env_big: one workgroup per env
+constexpr int kBigMaxV = 20 * kBigMaxThreads;
+constexpr int kBigStaticLds = 12 * 1024;  // Tables + BigShared
 __global__ void k_reset(EnvParams p, const int64_t *seeds, const uint8_t *env_mask, float *obs);
 __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double *vm_mem,
                          double *cpu, double *mem, int64_t *remaining, int64_t *rank);
@@ -95,6 +103,7 @@ struct vmp_handle {
   PoisConst *pois_dev;
   uint64_t *stamps;
   uint64_t *jump_dev;
+  bool big;  // k_env_big (V > 1024, or VMP_BIG_KERNEL=1)
   // eval-mode Record metrics (vmp_record.hip), allocated by vmp_record_enable
   bool rec_on;
   RecArgs rec;
@@ -211,7 +220,21 @@ int launch_env(vmp_handle *h, const StepOut &o) {
   const int64_t pre = 20 * (int64_t)p.scap + 4 * (int64_t)(o.k_steps > 0 ? o.k_steps : 1);
   p.lds_wave_bytes = (int32_t)align16(p.off_pre + pre);
   size_t lds = (size_t)p.lds_wave_bytes * kEnvWavesPerBlock;
-  if (lds > 160 * 1024 - 2048) return fail(VMP_EINVAL, "config too large for the LDS carve");
+  if (!h->big && lds > 160 * 1024 - 2048) return fail(VMP_EINVAL, "config too large for the LDS carve");
+  if (h->big) {
+    // one workgroup per env: the fewest slots per thread that fit 1024 threads
+    const int spt = h->V <= 4 * kBigMaxThreads ? 4
+                    : h->V <= 8 * kBigMaxThreads ? 8
+                    : h->V <= 16 * kBigMaxThreads ? 16 : 20;
+    const int nt = 64 * ((h->V + 64 * spt - 1) / (64 * spt));
+    const size_t lds1 = (size_t)p.lds_wave_bytes;
+    if (spt == 4) hipLaunchKernelGGL(k_env_big<4>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
+    else if (spt == 8) hipLaunchKernelGGL(k_env_big<8>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
+    else if (spt == 16) hipLaunchKernelGGL(k_env_big<16>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
+    else hipLaunchKernelGGL(k_env_big<20>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
+    HIP_TRY(hipGetLastError());
+    return VMP_OK;
+  }
   const int need = (h->V + 63) / 64;
   if (o.k_steps == 1) launch_vpt<true>(need, grid, block, lds, h->stream, p, o);
   else launch_vpt<false>(need, grid, block, lds, h->stream, p, o);
@@ -242,8 +265,8 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
                vmp_handle **out) {
   if (!cfg || !out || n_env <= 0 || !seeds) return fail(VMP_EINVAL, "null argument or n_env <= 0");
   if (cfg->pms < 1 || cfg->pms > 65533) return fail(VMP_EINVAL, "pms must be in [1, 65533]");
-  if (cfg->vms < 1 || cfg->vms > kMaxVPT * kWaveSize)
-    return fail(VMP_EINVAL, "vms must be in [1, 1024] on this build");
+  if (cfg->vms < 1 || cfg->vms > kBigMaxV)
+    return fail(VMP_EINVAL, "vms must be in [1, 10240] on this build");
   if (cfg->reward_function < 0 || cfg->reward_function > 2)
     return fail(VMP_EINVAL, "Function does not exist: reward_function");  // env.py:156
   if (cfg->sequence < 0 || cfg->sequence > 2) return fail(VMP_EINVAL, "unknown sequence");
@@ -261,6 +284,10 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   h->A = cfg->allow_null_action ? cfg->pms + 2 : cfg->pms + 1;
   h->D = 3 * cfg->vms + 2 * cfg->pms;
   h->W32 = (h->A + 31) / 32;
+  {
+    const char *force = getenv("VMP_BIG_KERNEL");
+    h->big = cfg->vms > kMaxVPT * kWaveSize || (force && force[0] == '1');
+  }
   h->device = device;
   h->stream = nullptr;
   std::vector<double> t1, t2;
@@ -326,14 +353,17 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   int maxn = h->V > h->P ? h->V : h->P;
   int depth = 0;
   for (int n = 0; n <= maxn; n++) depth = pw_depth(n) > depth ? pw_depth(n) : depth;
-  if (depth > 5) {
+  if (depth > 12) {
     vmp_destroy(h);
     return fail(VMP_EINVAL, "config exceeds the pairwise-sum recursion depth of this build");
   }
-  if ((p.lds_wave_bytes + 20 * kSpecDraws + 4 * kMaxStepsPerLaunch) * kWavesPerBlock >
-      160 * 1024 - 2048) {
-    vmp_destroy(h);
-    return fail(VMP_EINVAL, "config too large for the LDS carve of this build");
+  {
+    const int64_t per_env = p.lds_wave_bytes + 20 * kSpecDraws + 4 * kMaxStepsPerLaunch;
+    const int64_t need = h->big ? per_env + kBigStaticLds : per_env * kEnvWavesPerBlock + 2048;
+    if (need > 160 * 1024) {
+      vmp_destroy(h);
+      return fail(VMP_EINVAL, "config too large for the LDS carve of this build");
+    }
   }
   refresh_params(h);
   int64_t *dseeds = nullptr;
@@ -585,8 +615,12 @@ int vmp_get_counters(vmp_handle *h, int64_t *counters) {
 
 int vmp_get_stats(vmp_handle *h, double *stats) {
   if (!h || !stats) return fail(VMP_EINVAL, "null argument");
-  hipLaunchKernelGGL(k_target_means, dim3((h->N + kWavesPerBlock - 1) / kWavesPerBlock),
-                     dim3(64 * kWavesPerBlock), 0, h->stream, h->prm);
+  if (h->V > kMaxVPT * kWaveSize)  // beyond the static per-wave buffers: the env carve
+    hipLaunchKernelGGL(k_target_means_lds, dim3(h->N), dim3(64), (size_t)h->prm.lds_wave_bytes,
+                       h->stream, h->prm);
+  else
+    hipLaunchKernelGGL(k_target_means, dim3((h->N + kWavesPerBlock - 1) / kWavesPerBlock),
+                       dim3(64 * kWavesPerBlock), 0, h->stream, h->prm);
   hipLaunchKernelGGL(k_counters, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,
                      nullptr, stats);
   HIP_TRY(hipGetLastError());
@@ -605,8 +639,8 @@ int vmp_get_state(vmp_handle *h, int64_t *placement, double *vm_cpu, double *vm_
 
 int vmp_get_rank(vmp_handle *h, int64_t *rank) {
   if (!h || !rank) return fail(VMP_EINVAL, "null argument");
-  hipLaunchKernelGGL(k_export, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,
-                     nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, rank);
+  hipLaunchKernelGGL(k_rank, dim3(h->N), dim3(64), sizeof(uint64_t) * ((h->P + 63) / 64),
+                     h->stream, h->prm, rank);
   HIP_TRY(hipGetLastError());
   return VMP_OK;
 }

@@ -1737,4 +1737,692 @@ __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, ui
   mask[i] = (bits[r * W + (a >> 5)] >> (a & 31)) & 1u;
 }
 
+
+// ------------------------------------------------------- large-V env kernel
+// V > 1024 (e.g. the P1000 / V10000 stress config): one workgroup of NT =
+// 64 * NWV threads per env. Thread t holds VM slots v = s*NT + t (s < SPT) in
+// registers, so slot order (s, t) is ascending VM order. PM-level work (fit
+// bitmaps, BF sort, placements, frees, RNG draws, pairwise sums, reward) runs
+// on wave 0 with the wave kernel's helpers; per-VM events that the reference
+// applies in VM order are compacted across the block (bcx_rank, ascending t
+// within each s) and applied by wave 0 in that order. Same arithmetic, same
+// order as k_env: the two kernels are interchangeable (VMP_BIG_KERNEL=1
+// forces this one for any V, which the parity tests use).
+struct BigShared {
+  int32_t wcnt[16];   // per-wave counts of a compaction
+  int32_t bc[8];      // broadcast scalars
+  int64_t b64[4];
+  uint32_t evw[512];  // event list (one slot row of the block): VM word
+  int32_t evt[512];   // event list: target / value
+  uint8_t evok[512];  // event results
+};
+
+// Rank of this thread's flag among the flagged threads of the block
+// (ascending t) and the block total. Two barriers.
+__device__ __forceinline__ int bcx_rank(bool flag, BigShared &B, int &total) {
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const uint64_t m = ballot(flag);
+  __syncthreads();
+  if (lane == 0) B.wcnt[wid] = __popcll(m);
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int i = 0; i < nwv; i++) {
+    const int c = B.wcnt[i];
+    off += i < wid ? c : 0;
+    tot += c;
+  }
+  total = tot;
+  return off + below(m, lane);
+}
+
+__device__ __forceinline__ int block_sum_int(int x, BigShared &B) {
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  __syncthreads();
+  if (lane == 0) B.wcnt[wid] = x;
+  __syncthreads();
+  int s = 0;
+  for (int i = 0; i < nwv; i++) s += B.wcnt[i];
+  return s;
+}
+
+__device__ __forceinline__ int block_min_int(int x, BigShared &B) {
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
+  __syncthreads();
+  if (lane == 0) B.wcnt[wid] = x;
+  __syncthreads();
+  int s = 0x7fffffff;
+  for (int i = 0; i < nwv; i++) s = min(s, B.wcnt[i]);
+  return s;
+}
+
+// FirstFit / BestFit act fused with the action phase (heuristic_apply, block form).
+template <int SPT>
+__device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &L, const Tables &T,
+                                                 BigShared &B, uint32_t (&wa)[SPT], int policy,
+                                                 int32_t *act_out, uint8_t *valid_out) {
+  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+  const bool w0 = t < 64;
+  const int P = p.P, WAIT = p.P, NW = p.NW;
+  const bool bf = policy == 1;
+  uint32_t pend = 0;
+#pragma unroll 1
+  for (int s = 0; s < SPT; s++)
+    if (w_pl(wa[s]) == WAIT) pend |= 1u << s;
+  uint32_t won = 0, bad = 0;
+  int64_t n_place = 0;
+  if (block_sum_int(pend != 0, B) > 0) {
+    if (w0) {
+      for (int i = lane; i < P; i += 64) {
+        const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
+        L.fcpu[i] = fcv;
+        L.fmem[i] = fmv;
+        L.tc[i] = (uint8_t)(fit_threshold(fcv) + 1);
+        L.tm[i] = (uint8_t)(fit_threshold(fmv) + 1);
+      }
+      wsync();
+    }
+    bool rebuild = true;
+    uint32_t hit = 0;
+#pragma unroll 1
+    for (;;) {
+      if (rebuild) {
+        __syncthreads();
+        if (w0) {
+          if (bf) bf_sort(p, L);
+          build_bitmaps(p, L, bf);
+        }
+        __syncthreads();
+        hit = 0;
+#pragma unroll 1
+        for (int s = 0; s < SPT; s++)
+          if (((pend >> s) & 1u) && bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) >= 0)
+            hit |= 1u << s;
+        rebuild = false;
+      }
+      // earliest VM (index order) with a fit
+      int mine = 0x7fffffff;
+#pragma unroll 1
+      for (int s = SPT - 1; s >= 0; s--)
+        if ((hit >> s) & 1u) mine = s * NT + t;
+      const int vw = block_min_int(mine, B);
+      if (vw == 0x7fffffff) break;
+#pragma unroll 1
+      for (int s = 0; s < SPT; s++)
+        if (s * NT + t <= vw) pend &= ~(1u << s);
+      hit &= pend;
+      const int ws = vw / NT, wt = vw - ws * NT;
+      if (t == wt) {
+#pragma unroll 1
+        for (int s = 0; s < SPT; s++)
+          if (s == ws) B.bc[0] = (int32_t)wa[s];
+      }
+      __syncthreads();
+      const uint32_t ww = (uint32_t)B.bc[0];
+      const int kc = w_cc(ww), km = w_cm(ww);
+      if (w0) {
+        const int wpos = bm_query(L, NW, kc, km);
+        const int q = bf ? (int)L.ord[wpos] : wpos;
+        const bool ok = env_place(L, T, q, kc, km);
+        const int tc_old = (int)L.tc[q] - 1;
+        wsync();
+        if (lane == 0) {
+          const float nc = L.fcpu[q] + T.fcent[kc];
+          L.fcpu[q] = nc;
+          L.tc[q] = (uint8_t)(fit_threshold(nc) + 1);
+          if (bf) {
+            const float nm = L.fmem[q] + T.fcent[km];
+            L.fmem[q] = nm;
+            L.tm[q] = (uint8_t)(fit_threshold(nm) + 1);
+          }
+        }
+        wsync();
+        if (!bf) {  // only PM q's bit changes, for sizes above its new threshold
+          const int tq = (int)L.tc[q] - 1;
+          const int w = q >> 6;
+          const uint64_t bit = 1ull << (q & 63);
+          for (int k = lane; k < 101; k += 64) {
+            const uint64_t x = L.bc[k * NW + w];
+            L.bc[k * NW + w] = (tq >= k) ? (x | bit) : (x & ~bit);
+          }
+          wsync();
+        }
+        if (lane == 0) {
+          B.bc[1] = q;
+          B.bc[2] = ok;
+          B.bc[3] = tc_old;
+          B.bc[4] = (int)L.tc[q] - 1;
+          B.bc[5] = (int)L.tm[q] - 1;
+        }
+      }
+      __syncthreads();
+      const int q = B.bc[1];
+      const bool ok = B.bc[2] != 0;
+      n_place += ok;
+      if (t == wt) {
+#pragma unroll 1
+        for (int s = 0; s < SPT; s++)
+          if (s == ws) {
+            won |= 1u << s;
+            if (ok) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)q;
+            else bad |= 1u << s;
+          }
+        if (act_out) act_out[vw] = q;
+      }
+      if (bf) {
+        rebuild = true;
+      } else {  // re-query the VMs q fitted before and not after
+        const int tq = B.bc[4], tc_old = B.bc[3], tmq = B.bc[5];
+#pragma unroll 1
+        for (int s = 0; s < SPT; s++) {
+          const int c = w_cc(wa[s]);
+          if (((hit >> s) & 1u) && c > tq && c <= tc_old && w_cm(wa[s]) <= tmq &&
+              bm_query(L, NW, c, w_cm(wa[s])) < 0)
+            hit &= ~(1u << s);
+        }
+      }
+    }
+  }
+  if (act_out || valid_out) {
+#pragma unroll 1
+    for (int s = 0; s < SPT; s++) {
+      const int v = s * NT + t;
+      if (live(wa[s])) {
+        if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(wa[s]);
+        if (valid_out) valid_out[v] = (uint8_t)!((bad >> s) & 1u);
+      }
+    }
+  }
+  __syncthreads();
+  return n_place;
+}
+
+// External actions (external_apply, block form): per slot row s, the events
+// are compacted in ascending VM order and applied by wave 0 one by one.
+template <int SPT>
+__device__ __forceinline__ void big_external(const EnvParams &p, const Lds &L, const Tables &T,
+                                             BigShared &B, uint32_t (&wa)[SPT],
+                                             const int32_t *act_row, uint8_t *valid_out,
+                                             int64_t &n_place, int64_t &n_susp) {
+  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+  const int P = p.P, WAIT = p.P;
+#pragma unroll 1
+  for (int s = 0; s < SPT; s++) {
+    const int v = s * NT + t;
+    const bool in = live(wa[s]);
+    const int c = w_pl(wa[s]);
+    const int tg = in ? act_row[v] : c;
+    const bool isplace = in && c == WAIT && tg >= 0 && tg < P;
+    const bool issusp = in && c < P && tg == WAIT;
+    int nev = 0;
+    const int r = bcx_rank(isplace || issusp, B, nev);
+    if (isplace || issusp) {
+      B.evw[r] = wa[s];
+      B.evt[r] = tg;
+    }
+    __syncthreads();
+    if (t < 64) {
+#pragma unroll 1
+      for (int i = 0; i < nev; i++) {  // ascending VM index
+        const uint32_t ew = B.evw[i];
+        const int et = B.evt[i];
+        const int ec = w_pl(ew);
+        const double vc = T.cent[w_cc(ew)], vm = T.cent[w_cm(ew)];
+        const int q = (ec == WAIT) ? et : ec;
+        double cq = L.cpu[q], mq = L.mem[q];
+        bool eok = true;
+        if (ec == WAIT) {
+          eok = (cq + vc <= 1) && (mq + vm <= 1);
+          if (eok) {
+            cq = cq + vc;
+            mq = mq + vm;
+          }
+        } else {
+          cq = cq - vc;
+          mq = mq - vm;
+        }
+        wsync();
+        if (lane == 0) {
+          L.cpu[q] = cq;
+          L.mem[q] = mq;
+          B.evok[i] = (uint8_t)eok;
+        }
+        wsync();
+      }
+    }
+    __syncthreads();
+    bool ok = (tg == c) || issusp;
+    if (isplace) ok = B.evok[r] != 0;
+    n_place += block_sum_int(isplace && ok, B);
+    n_susp += block_sum_int(issusp, B);
+    if (ok && tg != c && in) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)tg;
+    if (valid_out && in) valid_out[v] = (uint8_t)ok;
+  }
+}
+
+// Wave 0 of k_env_big: the step's pairwise sums, reward, counters and
+// termination (env_tail's stats section); out of line so its temporaries do not
+// share the register budget with the block's slot arrays.
+__device__ __noinline__ void big_stats(const EnvParams &p, const Tables &T, BigShared &B,
+                                       char LDSP *base, int64_t k, int n_ex, int n_w,
+                                       int64_t n_term, int64_t arrivals) {
+  const Lds L = make_lds(p, base);
+  const int lane = lane_id();
+  const int P = p.P;
+  const bool kl = p.reward == 2;
+  EnvHdr LDSP *H = L.hdr;
+  double reward = 0.0;
+  {
+    double LDSP *res = L.jobres;
+    const double *cent = T.cent;
+    {
+#pragma unroll 1
+      for (int j = (k > 0 ? 0 : 2); j < (kl ? 4 : 2); j++) {
+        const uint8_t LDSP *src = (j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp);
+        const int n = j < 2 ? (int)k : n_ex;
+        const double r = wave_pw_sum(n, [=](int i) { return cent[src[i]]; }, L.pw);
+        wsync();
+        if (lane == 0) res[j] = r;
+        wsync();
+      }
+    }
+    if (p.reward >= 1) {
+      const int jend = p.reward == 2 ? 8 : 6;
+#pragma unroll 1
+      for (int j = 4; j < jend; j++) {
+        const double LDSP *src = (j & 1) ? L.mem : L.cpu;
+        const double mean = j < 6 ? 0.0 : res[j - 2] / (double)P;
+        const bool sq = j >= 6;
+        const double r = wave_pw_sum(P, [=](int i) {
+          const double x = src[i];
+          const double d = x - mean;
+          return sq ? d * d : x;
+        }, L.pw);
+        wsync();
+        if (lane == 0) res[j] = r;
+        wsync();
+      }
+    }
+    if (p.reward == 2) {
+#pragma unroll 1
+      for (int j = 8; j < 10; j++) {
+        const uint8_t LDSP *src = (j & 1) ? L.mcomp : L.ccomp;
+        const double mean = res[j - 6] / (double)n_ex;
+        const double r = wave_pw_sum(n_ex, [=](int i) {
+          const double d = cent[src[i]] - mean;
+          return d * d;
+        }, L.pw);
+        wsync();
+        if (lane == 0) res[j] = r;
+        wsync();
+      }
+    }
+    const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
+    if (!kl) res[2] = res[3] = 0.0;
+    double tcm = res[2] / (double)P;
+    if (p.cap_target_util && tcm > 1) tcm = 1.0;
+    double tmm = res[3] / (double)P;
+    if (p.cap_target_util && tmm > 1) tmm = 1.0;
+    if (n_ex > 0) {
+      if (p.reward == 2) {
+        double cv = res[6] / (double)P, mv = res[7] / (double)P;
+        if (cv == 0) cv = 1e-6;
+        if (mv == 0) mv = 1e-6;
+        double tcv = res[8] / (double)n_ex, tmv = res[9] / (double)n_ex;
+        if (tcv == 0) tcv = 1e-6;
+        if (tmv == 0) tmv = 1e-6;
+        reward = (tcm == 0 || tmm == 0)
+                     ? 0.0
+                     : kl_reward(tcm, tmm, tcv, tmv, res[4] / (double)P, res[5] / (double)P, cv, mv);
+      } else if (p.reward == 1) {
+        reward = p.beta * res[4] + (1 - p.beta) * res[5];
+      } else {
+        reward = -wr;
+      }
+    }
+    const int64_t ts = H->timestep;
+    const bool term = ts >= p.limit;
+    wsync();
+    if (lane == 0) {
+      H->timestep = ts + 1;
+      H->total_requests += arrivals;
+      H->served += n_term;
+      H->dropped += arrivals - k;
+      H->waiting_ratio = wr;
+      if (kl) {
+        H->tcm = tcm;
+        H->tmm = tmm;
+      }
+      if (k > 0) {
+        H->total_cpu_req = H->total_cpu_req + res[0];
+        H->total_mem_req = H->total_mem_req + res[1];
+      }
+      B.b64[0] = __double_as_longlong(reward);
+      B.bc[6] = term;
+    }
+    wsync();
+  }
+}
+
+__device__ __noinline__ void big_predraw(const EnvParams &p, const Tables &T, char LDSP *base,
+                                         int K, const uint64_t *jt) {
+  const Lds L = make_lds(p, base);
+  const U128 JA{jt[0], jt[1]}, JM{jt[2], jt[3]};
+  predraw(p, L, T, K, p.V, JA, JM);
+}
+
+// _run_vms, _accept_vm_requests, stats + reward, termination (env_tail, block form).
+template <int SPT>
+__device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, const Tables &T,
+                                           BigShared &B, uint32_t (&wa)[SPT],
+                                           uint32_t (&rem)[SPT], int kstep, bool &terminated) {
+  const int t = threadIdx.x, lane = lane_id();
+  const bool w0 = t < 64;
+  const int P = p.P, WAIT = p.P, NUL = p.P + 1;
+  EnvHdr LDSP *H = L.hdr;
+  // ---- _run_vms ----
+  int64_t n_term = 0;
+#pragma unroll 1
+  for (int s = 0; s < SPT; s++) {
+    const bool running = w_pl(wa[s]) < P;
+    if (running && rem[s] > 0) rem[s] -= 1;
+    const bool term = running && rem[s] == 0;
+    int nt = 0;
+    const int r = bcx_rank(term, B, nt);
+    if (term) B.evw[r] = wa[s];
+    __syncthreads();
+    if (w0) {
+#pragma unroll 1
+      for (int i = 0; i < nt; i++) {  // frees in ascending VM order
+        const uint32_t ew = B.evw[i];
+        const int q = w_pl(ew);
+        const double cq = L.cpu[q] - T.cent[w_cc(ew)];
+        const double mq = L.mem[q] - T.cent[w_cm(ew)];
+        wsync();
+        if (lane == 0) {
+          L.cpu[q] = cq;
+          L.mem[q] = mq;
+        }
+        wsync();
+      }
+    }
+    n_term += nt;
+    if (term) {
+      wa[s] = w_make(NUL, 0, 0);
+      rem[s] = 0;
+    }
+  }
+  __syncthreads();
+  if (w0)
+    for (int i = lane; i < P; i += 64) {  // precision clamp
+      if (L.cpu[i] < 1e-7) L.cpu[i] = 0;
+      if (L.mem[i] < 1e-7) L.mem[i] = 0;
+    }
+  // ---- _accept_vm_requests: the first k NULL slots in VM order ----
+  int n_null = 0;
+  int nrank[SPT];
+#pragma unroll 1
+  for (int s = 0; s < SPT; s++) {
+    const bool isnull = w_pl(wa[s]) == NUL;
+    int nn = 0;
+    const int r = bcx_rank(isnull, B, nn);
+    nrank[s] = isnull ? n_null + r : 0x7fffffff;
+    n_null += nn;
+  }
+  const int64_t arrivals = L.arr[kstep];
+  const int64_t k = arrivals < n_null ? arrivals : n_null;
+  __syncthreads();
+  if (k > 0) {
+    Pcg r1 = ld_pcg(H, 0), r2 = ld_pcg(H, 1);
+#pragma unroll 1
+    for (int64_t j0 = 0; j0 < k; j0 += 512) {
+      const int64_t j1 = j0 + 512 < k ? j0 + 512 : k;
+      if (w0) {
+#pragma unroll 1
+        for (int64_t j = j0; j < j1; j++) {
+          const int cc = (int)rint((p.seq_lo + p.seq_range * next_double(r1)) * 100.0);
+          const int cm = (int)rint((p.seq_lo + p.seq_range * next_double(r2)) * 100.0);
+          const uint32_t rr = svc_take(p, L);
+          if (lane == 0) {
+            L.accc[j] = (uint8_t)cc;
+            L.accm[j] = (uint8_t)cm;
+            B.evt[j - j0] = (int32_t)rr;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll 1
+      for (int s = 0; s < SPT; s++) {
+        const int j = nrank[s];
+        if (j >= j0 && j < j1) {
+          wa[s] = w_make(WAIT, L.accc[j], L.accm[j]);
+          rem[s] = (uint32_t)B.evt[j - j0];
+        }
+      }
+      __syncthreads();
+    }
+    if (w0) {
+      st_pcg(H, 0, r1);
+      st_pcg(H, 1, r2);
+    }
+  }
+  __syncthreads();
+  // ---- stats + reward ----
+  const bool kl = p.reward == 2;
+  int n_ex = 0, n_w = 0;
+#pragma unroll 1
+  for (int s = 0; s < SPT; s++) {
+    const int c = w_pl(wa[s]);
+    const bool ex = c <= WAIT;
+    int ne = 0;
+    const int r = bcx_rank(ex, B, ne);
+    if (kl && ex) {
+      L.ccomp[n_ex + r] = (uint8_t)w_cc(wa[s]);
+      L.mcomp[n_ex + r] = (uint8_t)w_cm(wa[s]);
+    }
+    n_ex += ne;
+    n_w += c == WAIT;
+  }
+  n_w = block_sum_int(n_w, B);
+  __syncthreads();
+  if (w0) big_stats(p, T, B, L.base, k, n_ex, n_w, n_term, arrivals);
+  __syncthreads();
+  const double reward = __longlong_as_double(B.b64[0]);
+  terminated = B.bc[6] != 0;
+  __syncthreads();
+  return reward;
+}
+
+template <int SPT>
+__global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
+  extern __shared__ __align__(16) char lds[];
+  __shared__ Tables T;
+  __shared__ BigShared B;
+  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+  const bool w0 = t < 64;
+  const int e = blockIdx.x;
+  const Lds L = make_lds(p, (char LDSP *)lds);
+  const int V = p.V, P = p.P;
+  for (int i = t; i < 128; i += NT) {
+    T.cent[i] = (double)i / 100.0;
+    T.fcent[i] = (float)((double)i / 100.0);
+  }
+  constexpr int kPoisWords = (int)(2 * sizeof(PoisConst) / 4);
+  if (t < kPoisWords) reinterpret_cast<uint32_t *>(T.pois)[t] = reinterpret_cast<const uint32_t *>(p.pois)[t];
+  if (t < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[t] = reinterpret_cast<const uint64_t *>(p.hdr + e)[t];
+  const double *pm = p.pm + (int64_t)e * 2 * P;
+  for (int i = t; i < 2 * P; i += NT) L.cpu[i] = pm[i];
+  const uint64_t *vmw = p.vmw + (int64_t)e * V;
+  uint32_t wa[SPT], rem[SPT];
+#pragma unroll 1
+  for (int s = 0; s < SPT; s++) {
+    const int v = s * NT + t;
+    const uint64_t w = v < V ? vmw[v] : (uint64_t)kPad;
+    wa[s] = (uint32_t)w;
+    rem[s] = (uint32_t)(w >> 32);
+  }
+  __syncthreads();
+  if (o.k_steps > 0 && w0) {
+    const uint64_t *jt = p.jump + 4 * lane;
+    big_predraw(p, T, L.base, o.k_steps, jt);
+  }
+  __syncthreads();
+  bool term = false;
+  int64_t ndone = 0;
+#pragma unroll 1
+  for (int k = 0; k < o.k_steps; k++) {
+    const bool last = k == o.k_steps - 1;
+    uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
+    int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
+    int64_t n_place = 0, n_susp = 0;
+    if (o.policy >= 0)
+      n_place = big_heuristic<SPT>(p, L, T, B, wa, o.policy, act_row, valid_row);
+    else
+      big_external<SPT>(p, L, T, B, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
+    __syncthreads();
+    if (t == 0) {
+      L.hdr->place_action += n_place;
+      L.hdr->suspend_action += n_susp;
+    }
+    __syncthreads();
+    const double r = big_tail<SPT>(p, L, T, B, wa, rem, k, term);
+    if (o.reward && t == 0) o.reward[(int64_t)k * p.N + e] = r;
+    ndone += term;
+  }
+  if (o.k_steps > 0) {
+    if (w0) svc_commit(L);
+  }
+  if (o.k_steps == 0 && o.policy >= 0 && o.act_out) {
+    uint32_t wt[SPT];
+#pragma unroll 1
+    for (int s = 0; s < SPT; s++) wt[s] = wa[s];
+    big_heuristic<SPT>(p, L, T, B, wt, o.policy, o.act_out + (int64_t)e * V, nullptr);
+  }
+  __syncthreads();
+  if (o.obs) {
+    float *obs = o.obs + (int64_t)e * p.D;
+#pragma unroll 1
+    for (int s = 0; s < SPT; s++) {
+      const int v = s * NT + t;
+      if (live(wa[s])) {
+        ST_NT(obs + v, (float)w_pl(wa[s]));
+        ST_NT(obs + V + v, T.fcent[w_cc(wa[s])]);
+        ST_NT(obs + 2 * V + v, T.fcent[w_cm(wa[s])]);
+      }
+    }
+    for (int i = t; i < P; i += NT) {
+      ST_NT(obs + 3 * V + i, (float)L.cpu[i]);
+      ST_NT(obs + 3 * V + P + i, (float)L.mem[i]);
+    }
+  }
+  if (o.mask_bits) {
+    uint32_t *bits = o.mask_bits + (int64_t)e * V * p.W32;
+    const int A = p.A, W = p.W32, WAIT = p.P, NUL = p.P + 1;
+#pragma unroll 1
+    for (int s = 0; s < SPT; s++) {
+      const int v = s * NT + t;
+      const bool in = live(wa[s]);
+      const int c = in ? w_pl(wa[s]) : NUL;
+      const double vc = T.cent[w_cc(wa[s])], vm = T.cent[w_cm(wa[s])];
+      const bool waiting = in && c == WAIT;
+#pragma unroll 1
+      for (int w = 0; w < W; w++) {
+        uint32_t word = 0xFFFFFFFFu;
+        const int a0 = w * 32;
+        if (c >= a0 && c < a0 + 32 && c < A) word &= ~(1u << (c - a0));
+        if (c < P && WAIT >= a0 && WAIT < a0 + 32) word &= ~(1u << (WAIT - a0));
+        if (waiting) {
+          const int hi = min(a0 + 32, P);
+#pragma unroll 1
+          for (int q = a0; q < hi; q++) {
+            const bool fit = (L.cpu[q] + vc <= 1) && (L.mem[q] + vm <= 1);
+            if (fit) word &= ~(1u << (q - a0));
+          }
+        }
+        if (in) bits[(int64_t)v * W + w] = word;
+      }
+    }
+  }
+  if (o.k_steps > 0) {
+    if (o.done && t == 0) o.done[e] = (uint8_t)term;
+    if (o.done_count && t == 0) o.done_count[e] += ndone;
+    uint64_t *vmo = p.vmw + (int64_t)e * V;
+#pragma unroll 1
+    for (int s = 0; s < SPT; s++) {
+      const int v = s * NT + t;
+      if (live(wa[s])) ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rem[s] << 32));
+    }
+    double *pmo = p.pm + (int64_t)e * 2 * P;
+    for (int i = t; i < 2 * P; i += NT) ST_NT(pmo + i, (double)L.cpu[i]);
+    if (t < 32)
+      reinterpret_cast<uint64_t *>(p.hdr + e)[t] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
+  }
+}
+template __global__ void k_env_big<4>(EnvParams, StepOut);
+template __global__ void k_env_big<8>(EnvParams, StepOut);
+template __global__ void k_env_big<16>(EnvParams, StepOut);
+template __global__ void k_env_big<20>(EnvParams, StepOut);
+
+// _get_rank for any V: one wave per env, LDS bitmap of used PMs.
+__global__ __launch_bounds__(64) void k_rank(EnvParams p, int64_t *rank) {
+  extern __shared__ unsigned long long used[];
+  const int lane = lane_id(), e = blockIdx.x;
+  const int NWP = (p.P + 63) / 64;
+  for (int i = lane; i < NWP; i += 64) used[i] = 0ull;
+  __syncthreads();
+  const uint64_t *row = p.vmw + (int64_t)e * p.V;
+  for (int v = lane; v < p.V; v += 64) {
+    const int st = (int)(row[v] & 0xFFFFu);
+    if (st < p.P) atomicOr(used + (st >> 6), 1ull << (st & 63));
+  }
+  __syncthreads();
+  int64_t r = 0;
+  for (int i = lane; i < NWP; i += 64) r += __popcll(used[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+  if (lane == 0) rank[e] = r;
+}
+
+// target means for any V: one wave per env on the env's LDS carve (ccomp /
+// mcomp and the pairwise-sum plan of make_lds).
+__global__ __launch_bounds__(64) void k_target_means_lds(EnvParams p) {
+  extern __shared__ __align__(16) char lds[];
+  __shared__ double cent[128];
+  for (int i = threadIdx.x; i < 128; i += 64) cent[i] = (double)i / 100.0;
+  __syncthreads();
+  const int lane = lane_id(), e = blockIdx.x;
+  const Lds L = make_lds(p, (char LDSP *)lds);
+  const int V = p.V, P = p.P;
+  const uint64_t *row = p.vmw + (int64_t)e * V;
+  int n_ex = 0;
+  for (int b = 0; b < V; b += 64) {
+    const int v = b + lane;
+    const uint64_t w = v < V ? row[v] : (uint64_t)(P + 1);
+    const bool ex = v < V && (int)(w & 0xFFFFu) <= P;
+    const uint64_t m = ballot(ex);
+    if (ex) {
+      const int rk = n_ex + below(m, lane);
+      L.ccomp[rk] = (uint8_t)((w >> 16) & 0xFFu);
+      L.mcomp[rk] = (uint8_t)((w >> 24) & 0xFFu);
+    }
+    n_ex += __popcll(m);
+  }
+  wsync();
+  const double *ct = cent;
+  const uint8_t LDSP *cc = L.ccomp;
+  const uint8_t LDSP *cm = L.mcomp;
+  const double sc = wave_pw_sum(n_ex, [=](int i) { return ct[cc[i]]; }, L.pw);
+  const double sm = wave_pw_sum(n_ex, [=](int i) { return ct[cm[i]]; }, L.pw);
+  if (lane == 0) {
+    double tcm = sc / (double)P, tmm = sm / (double)P;
+    if (p.cap_target_util && tcm > 1) tcm = 1.0;
+    if (p.cap_target_util && tmm > 1) tmm = 1.0;
+    p.hdr[e].tcm = tcm;
+    p.hdr[e].tmm = tmm;
+  }
+}
+
 }  // namespace vmp

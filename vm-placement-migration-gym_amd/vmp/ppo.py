@@ -65,6 +65,7 @@ class PPOConfig:
     device: str = "cpu"  # the reference's default; the build always uses the env's GPU
     # ---- build options (not in the reference) ----
     value_loss_broadcast: bool = True  # ppo.py:266-270 [mb,1]-[mb] broadcast
+    precision: str = "f32"             # "bf16": bf16 GEMM inputs, f32 accumulate/output
     chunk_bytes: int = 4 << 30         # logits budget per update chunk
     seed_stride: int = 4               # env/episode reset seed spacing
 
@@ -73,6 +74,44 @@ def ortho_init(layer, scale=np.sqrt(2)):
     nn.init.orthogonal_(layer.weight, gain=scale)
     nn.init.constant_(layer.bias, 0)
     return layer
+
+
+class BF16Linear(torch.autograd.Function):
+    """y = x W^T + b with bf16 GEMM inputs and f32 accumulation / output
+    (hipBLASLt through torch.mm(..., out_dtype=float32)); the backward GEMMs
+    likewise. Parameters and everything outside the GEMMs stay f32, and the
+    rounding of x and W is deterministic, so the rollout's and the update's
+    log-probabilities of the same sample agree to f32 accumulation noise."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xb, wb = x.to(torch.bfloat16), w.to(torch.bfloat16)
+        y = torch.mm(xb, wb.t(), out_dtype=torch.float32)
+        if b is not None:
+            y = y + b
+        ctx.save_for_backward(xb, wb)
+        ctx.has_bias = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xb, wb = ctx.saved_tensors
+        g = gy.to(torch.bfloat16)
+        gx = torch.mm(g, wb, out_dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        gw = torch.mm(g.t(), xb, out_dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+def _run_mlp(seq, x, precision):
+    if precision != "bf16":
+        return seq(x)
+    for m in seq:
+        if isinstance(m, nn.Linear):
+            x = BF16Linear.apply(x, m.weight, m.bias)
+        else:
+            x = m(x)
+    return x
 
 
 def _nvec(action_space):
@@ -103,9 +142,14 @@ class Network(nn.Module):
                        scale=0.01))
         self._head = head if head is not None else H.policy_head
         self.rng = H.HeadRng(torch.initial_seed() if seed is None else seed)
+        self.precision = "f32"
+
+    def actor_logits(self, obs):
+        """self.actor(obs), in the configured GEMM precision."""
+        return _run_mlp(self.actor, obs, self.precision)
 
     def get_value(self, obs):
-        return self.critic(obs)
+        return _run_mlp(self.critic, obs, self.precision)
 
     def head(self, logits, invalid_mask=None, action=None, wait_ratio=-1.0, wait_index=-1):
         """Masked head on precomputed logits -> (action int32 [B,V], logprob [B], entropy [B])."""
@@ -115,13 +159,13 @@ class Network(nn.Module):
 
     def get_action(self, obs, action=None, invalid_mask=None):
         """ppo.py:115-126 -> (action int64 [B,V], logprob [B], entropy [B])."""
-        logits = self.actor(obs)
+        logits = self.actor_logits(obs)
         act, lp, ent = self.head(logits, invalid_mask, action)
         return act.long(), lp, ent
 
     def get_det_action(self, obs, action=None):
         """ppo.py:128-131: argmax of the unmasked logits; [V] for one observation."""
-        logits = self.actor(obs)
+        logits = self.actor_logits(obs)
         a = H.det_action(logits, self.V, self.A).long()
         return a[0] if obs.dim() == 1 or obs.shape[0] == 1 else a
 
@@ -183,6 +227,9 @@ class PPOAgent(Base):
         nvec = np.full(self.benv.V, self.benv.A, dtype=np.int64)
         self.model = Network(self.obs_dim, nvec, self.config.hidden_size, self.float_dtype,
                              head=self._head_impl).to(self.device)
+        if self.config.precision not in ("f32", "bf16"):
+            raise ValueError(f"precision must be 'f32' or 'bf16', not {self.config.precision!r}")
+        self.model.precision = self.config.precision
         self.optimizer = torch.optim.AdamW(self.model.parameters(), lr=self.config.lr)
 
     def eval(self, mode=True):
@@ -213,14 +260,14 @@ class PPOAgent(Base):
             bits = None
             if self.config.masked:
                 bits = self._coin_flip_bits(self.benv.mask_bits()[:1])
-            act, _, _ = self.model.head(self.model.actor(o), bits)
+            act, _, _ = self.model.head(self.model.actor_logits(o), bits)
             return act.flatten().long().cpu().numpy()
 
     def act_batch(self, obs, bits=None):
         """PPOAgent.act for every env of the batch on the device: int32 [N, V].
         The WAIT coin flips use the head's counter-based stream."""
         with torch.no_grad():
-            logits = self.model.actor(obs)
+            logits = self.model.actor_logits(obs)
             if self.config.det:
                 return H.det_action(logits, self.benv.V, self.benv.A)
             if self.config.masked and bits is None:
@@ -379,7 +426,7 @@ class PPOTrainer:
             bits = None
             if self.bits is not None:
                 bits = env.mask_bits(out=self.bits[t])
-            logits = m.actor(o)
+            logits = m.actor_logits(o)
             act, lp, _ = m._head(logits, self.V, self.A, bits=bits, rng=m.rng)
             self.act[t].copy_(act)
             self.logp[t].copy_(lp)
@@ -462,7 +509,7 @@ class PPOTrainer:
                     o = obs[t0:t1, n0:n1].reshape(mt * nc, -1)
                     b = None if bits is None else bits[t0:t1, n0:n1].reshape(mt * nc, self.V, -1)
                     a = act[t0:t1, n0:n1].reshape(mt * nc, self.V)
-                    logits = m.actor(o)
+                    logits = m.actor_logits(o)
                     _, newlp, ent = m._head(logits, self.V, self.A, bits=b, action=a,
                                             rng=m.rng)
                     newlp = newlp.reshape(mt, nc)
