@@ -202,6 +202,7 @@ def main():
         ppo_train = _guard(bench_ppo_train, args, dev, rank, world, dist)
         ppo_train_bf16 = _guard(bench_ppo_train, args, dev, rank, world, dist, "bf16")
         ppo_eval = _guard(bench_ppo_eval, args, dev, rank, world, dist)
+    stress = None if args.no_ppo else _guard(bench_stress, args, dev, rank, world, dist)
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / K, "higher_is_better": True,
@@ -222,6 +223,7 @@ def main():
         "ppo_train": ppo_train,
         "ppo_train_bf16": ppo_train_bf16,
         "ppo_eval": ppo_eval,
+        "stress_p1000_v10000": stress,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -288,6 +290,44 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
             "minibatch_steps": st["minibatches"], "kl_breaks": st["kl_breaks"],
             "parallelism": f"data-parallel x{world} (RCCL grad all-reduce)" if world > 1
             else "single GPU"}
+
+
+def bench_stress(args, dev, rank, world, dist):
+    """BASELINE config 5: P1000 / V10000 at 100 % load
+    (lambda = 1000/0.55/1000), L = 1000, reward kl, BestFit act + step, 512 envs
+    per GPU on the block-per-env kernel; 100 fast-forward steps, then 10 timed."""
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp import _lib
+    P, V, N = 1000, 10000, 512
+    cfg = Config(pms=P, vms=V, arrival_rate=round(1000 / 0.55 / 1000, 3), service_length=1000,
+                 training_steps=10000, eval_steps=100000, seed=0, reward_function="kl",
+                 sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
+    env = BatchedVmEnv(cfg, N, seeds=4 * (rank * N + np.arange(N, dtype=np.int64)), device=dev)
+    env.rollout("bestfit", 100)
+    obs = torch.empty((N, env.D), dtype=torch.float32, device=dev)
+    rew = torch.empty((N,), dtype=torch.float64, device=dev)
+    done = torch.empty((N,), dtype=torch.uint8, device=dev)
+    L, h = _lib.lib(), env._bind()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    K = 10
+    t0 = time.perf_counter()
+    for _ in range(K):
+        _lib.check(L.vmp_heuristic_step(h, 1, None, _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done),
+                                        None))
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    env.close()
+    bpe = step_bytes(P, V)
+    return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
+            "workload": "P1000 V10000, lambda 1.818, L 1000, reward kl, BestFit act + step "
+                        "(k_env_big, one workgroup per env)", "envs_per_gpu": N,
+            "ms_per_step": 1e3 * el / K, "bytes_per_env_step": bpe,
+            "hbm_frac": bpe * N * K / el / (HBM_PEAK_GBS * 1e9)}
 
 
 def bench_ppo_eval(args, dev, rank, world, dist):
