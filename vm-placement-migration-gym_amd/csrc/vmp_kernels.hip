@@ -730,6 +730,50 @@ __device__ __forceinline__ void bf_sort(const EnvParams &p, const Lds &L) {
   wsync();
 }
 
+// BestFit's choice for sizes (kc, km) (bestfit.py:33-39): the first PM in
+// visiting order flip(argsort(fcpu + fmem)) that fits, i.e. the fitting PM of
+// largest key. Fast path: a wave argmax over the PMs; only when two or more
+// fitting PMs share the largest key does their order matter, and then the
+// scalar introsort (bf_sort, numpy's tie order) runs and the
+// first fitting visiting position is taken. Returns -1 if nothing fits.
+__device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int kc, int km) {
+  const int lane = lane_id();
+  const int P = p.P;
+  float best = -INFINITY;
+  int cnt = 0, bi = -1;
+  for (int i = lane; i < P; i += 64) {
+    if ((int)L.tc[i] - 1 >= kc && (int)L.tm[i] - 1 >= km) {
+      const float key = L.fcpu[i] + L.fmem[i];
+      if (key > best) {
+        best = key;
+        cnt = 1;
+        bi = i;
+      } else if (key == best) {
+        cnt++;
+      }
+    }
+  }
+  float m = best;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  int tot = (best == m) ? cnt : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  if (tot == 0) return -1;
+  if (tot == 1) {
+    const uint64_t who = ballot(best == m && cnt == 1);
+    return __builtin_amdgcn_readlane(bi, __ffsll((unsigned long long)who) - 1);
+  }
+  bf_sort(p, L);  // ties at the top: numpy's order decides
+  for (int b = 0; b < P; b += 64) {
+    const int i = b + lane;
+    const int q = i < P ? (int)L.ord[i] : 0;
+    const uint64_t f = ballot(i < P && (int)L.tc[q] - 1 >= kc && (int)L.tm[q] - 1 >= km);
+    if (f) return __builtin_amdgcn_readlane(q, __ffsll((unsigned long long)f) - 1);
+  }
+  return -1;
+}
+
 // One VM placement event of the env (env.py:74-84 for a WAIT -> PM move):
 // _resource_valid in f64, then _place_vm. Returns validity (wave-uniform).
 __device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int q, int kc, int km) {
@@ -962,7 +1006,8 @@ __device__ __forceinline__ void svc_commit(const Lds &L) {
 //  - after a FirstFit win on PM q only q's cpu threshold drops, so the cached
 //    "has a fit" bit of a later VM can change only if q fitted it before and
 //    not after (its first fit was then q or earlier; re-querying is exact
-//    either way); BestFit re-sorts, so it rebuilds and re-queries everything;
+//    either way); BestFit changes both of q's thresholds and re-queries the
+//    VMs q fitted before and not after; its target is bf_choose's argmax;
 //  - the heuristic's state (f32 view) and the env's state (f64) are disjoint,
 //    so applying each winner's env event as soon as it is decided equals
 //    deciding every action first and stepping afterwards (env.py:68-88).
@@ -994,9 +1039,8 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     uint32_t hit = 0;  // bit s: VM slot s of this lane is pending and some PM fits it
 #pragma unroll 1
     for (;;) {
-      if (rebuild) {  // single site: initial build, and BF's re-sort after a win
-        if (bf) bf_sort(p, L);
-        build_bitmaps(p, L, bf);
+      if (rebuild) {  // single site: the initial build (index-order fit bitmaps)
+        build_bitmaps(p, L, false);
         rebuild = false;
         STAMP(17);
         // which pending VMs have any fit: branch-free row ANDs for P <= 128
@@ -1043,8 +1087,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         if (s < ws || (s == ws && lane <= wl)) pend &= ~(1u << s);
       hit &= pend;
       const int kc = w_cc(ww), km = w_cm(ww);
-      const int wpos = bm_query(L, NW, kc, km);  // wave-uniform
-      const int q = bf ? (int)L.ord[wpos] : wpos;
+      const int q = bf ? bf_choose(p, L, kc, km) : bm_query(L, NW, kc, km);  // wave-uniform
       const bool ok = env_place(L, T, q, kc, km);  // env.py:55-56, 58-64
       n_place += ok;
       if (lane == wl) {
@@ -1058,7 +1101,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         if (act_out) act_out[ws * 64 + wl] = q;
       }
       // heuristic state update (f32): FF updates cpu only (firstfit.py:36)
-      const int tc_old = (int)L.tc[q] - 1;
+      const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
       wsync();
       if (lane == 0) {
         const float nc = L.fcpu[q] + T.fcent[kc];
@@ -1071,9 +1114,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         }
       }
       wsync();
-      if (bf) {
-        rebuild = true;
-      } else {  // only PM q's bit changes, for sizes above its new threshold
+      {  // only PM q's bits change (cpu row; BF also the memory row)
         const int t = (int)L.tc[q] - 1;
         const int tmq = (int)L.tm[q] - 1;
         const int w = q >> 6;
@@ -1081,15 +1122,19 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         for (int k = lane; k < 101; k += 64) {
           const uint64_t x = L.bc[k * NW + w];
           L.bc[k * NW + w] = (t >= k) ? (x | bit) : (x & ~bit);
+          if (bf) {
+            const uint64_t y = L.bm[k * NW + w];
+            L.bm[k * NW + w] = (tmq >= k) ? (y | bit) : (y & ~bit);
+          }
         }
         wsync();
         // re-query the VMs q fitted before and not after
 #pragma unroll
         for (int s = 0; s < VPT; s++) {
-          const int c = w_cc(wa[s]);
-          const bool rq = ((hit >> s) & 1u) && c > t && c <= tc_old && w_cm(wa[s]) <= tmq;
+          const int c = w_cc(wa[s]), m = w_cm(wa[s]);
+          const bool rq = ((hit >> s) & 1u) && c <= tc_old && m <= tm_old && !(c <= t && m <= tmq);
           if (ballot(rq)) {
-            if (rq && bm_query(L, NW, c, w_cm(wa[s])) < 0) hit &= ~(1u << s);
+            if (rq && bm_query(L, NW, c, m) < 0) hit &= ~(1u << s);
           }
         }
       }
@@ -1831,10 +1876,7 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
     for (;;) {
       if (rebuild) {
         __syncthreads();
-        if (w0) {
-          if (bf) bf_sort(p, L);
-          build_bitmaps(p, L, bf);
-        }
+        if (w0) build_bitmaps(p, L, false);
         __syncthreads();
         hit = 0;
 #pragma unroll 1
@@ -1864,10 +1906,9 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
       const uint32_t ww = (uint32_t)B.bc[0];
       const int kc = w_cc(ww), km = w_cm(ww);
       if (w0) {
-        const int wpos = bm_query(L, NW, kc, km);
-        const int q = bf ? (int)L.ord[wpos] : wpos;
+        const int q = bf ? bf_choose(p, L, kc, km) : bm_query(L, NW, kc, km);
         const bool ok = env_place(L, T, q, kc, km);
-        const int tc_old = (int)L.tc[q] - 1;
+        const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
         wsync();
         if (lane == 0) {
           const float nc = L.fcpu[q] + T.fcent[kc];
@@ -1880,13 +1921,17 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
           }
         }
         wsync();
-        if (!bf) {  // only PM q's bit changes, for sizes above its new threshold
-          const int tq = (int)L.tc[q] - 1;
+        {  // only PM q's bits change (cpu row; BF also the memory row)
+          const int tq = (int)L.tc[q] - 1, tmq = (int)L.tm[q] - 1;
           const int w = q >> 6;
           const uint64_t bit = 1ull << (q & 63);
           for (int k = lane; k < 101; k += 64) {
             const uint64_t x = L.bc[k * NW + w];
             L.bc[k * NW + w] = (tq >= k) ? (x | bit) : (x & ~bit);
+            if (bf) {
+              const uint64_t y = L.bm[k * NW + w];
+              L.bm[k * NW + w] = (tmq >= k) ? (y | bit) : (y & ~bit);
+            }
           }
           wsync();
         }
@@ -1896,6 +1941,7 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
           B.bc[3] = tc_old;
           B.bc[4] = (int)L.tc[q] - 1;
           B.bc[5] = (int)L.tm[q] - 1;
+          B.bc[7] = tm_old;
         }
       }
       __syncthreads();
@@ -1912,15 +1958,13 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
           }
         if (act_out) act_out[vw] = q;
       }
-      if (bf) {
-        rebuild = true;
-      } else {  // re-query the VMs q fitted before and not after
-        const int tq = B.bc[4], tc_old = B.bc[3], tmq = B.bc[5];
+      {  // re-query the VMs q fitted before and not after
+        const int tq = B.bc[4], tc_old = B.bc[3], tmq = B.bc[5], tm_old = B.bc[7];
 #pragma unroll 1
         for (int s = 0; s < SPT; s++) {
-          const int c = w_cc(wa[s]);
-          if (((hit >> s) & 1u) && c > tq && c <= tc_old && w_cm(wa[s]) <= tmq &&
-              bm_query(L, NW, c, w_cm(wa[s])) < 0)
+          const int c = w_cc(wa[s]), m = w_cm(wa[s]);
+          if (((hit >> s) & 1u) && c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) &&
+              bm_query(L, NW, c, m) < 0)
             hit &= ~(1u << s);
         }
       }
