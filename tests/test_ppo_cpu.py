@@ -219,3 +219,15 @@ def test_cli_parses_reference_yaml(tmp_path):
     assert a.config["agents"]["ppo"]["hidden_size"] == 512
     with pytest.raises(ValueError):
         make_agent("drlvmp", None, {})
+
+
+def test_suspension_grid_and_row_format():
+    """vmp.exp builds exp_suspension.py's grid and row layout (CPU: no env run)."""
+    from vmp.exp import Cell, suspension_config, suspension_row
+    c = suspension_config(0.7, 1000)
+    assert c["arrival_rate"] == 0.127 and c["reward_function"] == "wr" and c["vms"] == 300
+    s = {"total served VMs": 12592, "total suspend actions": 0, "total place actions": 12716,
+         "_mean_life": 994.4, "_mean_pending": 0.0251, "_mean_slowdown": 0.0,
+         "_max_slowdown": 0.0}
+    assert suspension_row(Cell("firstfit", 0.7, 1000), [s]) == \
+        "firstfit,0.7,1000,12592,0,12716,994,0.025,0.000,0.000"

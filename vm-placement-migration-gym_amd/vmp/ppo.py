@@ -190,6 +190,10 @@ class ActStepGraph:
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side), torch.no_grad():
+            # hipBLASLt sets up a GEMM shape on its first call, which is not
+            # allowed under capture: run the actor once even when warmup == 0
+            # (no env step, so the envs' state is untouched)
+            agent.model.actor_logits(self.obs.to(agent.float_dtype))
             for _ in range(warmup):
                 self._step()
         torch.cuda.current_stream(dev).wait_stream(side)
