@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 3
+#define VMP_ABI_VERSION 4
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -63,7 +63,14 @@ extern "C" {
 #define VMP_REC_REWARD_OK 13 /* sum and count of rewards > -1e7, count of rewards < -1e7 */
 #define VMP_REC_N_OK 14
 #define VMP_REC_N_BAD 15
-#define VMP_NREC 16
+#define VMP_REC_CPUVAR 16   /* sum over steps of var over PMs of cpu, of memory */
+#define VMP_REC_MEMVAR 17   /*   (exp_performance.py:109-113, exp_vm_size.py:78-83) */
+#define VMP_REC_XMEM 18     /* sum over steps and PMs of mem[e][p] * sum_s mem[s][p] over the
+                               handle's envs: their sum over e is the cross-env square
+                               exp_performance.py:114 (np.var(memory, axis=0)) needs; 0 when
+                               n_env > VMP_REC_XMAX */
+#define VMP_NREC 19
+#define VMP_REC_XMAX 64
 #define VMP_REC_BINS 1001   /* pending / slowdown rates x1000: 0 .. 1000 */
 /* actor-head modes (vmp_policy_head) */
 #define VMP_HEAD_SAMPLE 0 /* Network.get_action(obs, action=None, mask) (ppo.py:115-126) */

@@ -43,3 +43,45 @@ def test_suspension_sweep_ppo_cell(tmp_path):
     name, load, sr, served, susp, valid = rows[0].split(",")[:6]
     assert name == "ppo-test" and load == "1.0" and sr == "1000"
     assert int(valid) >= int(susp) >= 0 and int(served) >= 0
+
+
+def _summary(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return [",".join(x.strip() for x in r) for r in csv.reader(f)][1:]
+
+
+# exp_performance's published load-1.0 rows carry the wr return (their other
+# columns do not depend on the reward), the load-0.6 rows the ut return: each
+# cell runs with the reward that printed its row.
+def test_performance_rows_match_published():
+    """data/exp_performance/summary.csv, heuristic rows: config/100.yml at
+    100 % and 60 % load, 5 seeds x 100 000 eval steps per row, every column
+    (return, drop rate, served, CPU/memory mean and variance incl. the
+    reference's variance-over-seeds memory column, pending, waiting, slowdown)."""
+    from vmp import exp
+    pub = {tuple(r.split(",")[:2]): r for r in _summary("exp_performance_summary.csv")}
+    cells = [exp.performance_cell(ag, ag, ld, "wr" if ld == 1.0 else "ut")
+             for ld in (1.0, 0.6) for ag in ("bestfit", "firstfit")]
+    rows = exp.performance_sweep(cells)
+    for row in rows:
+        assert row == pub[tuple(row.split(",")[:2])], row
+
+
+def test_performance_small_rows_match_published():
+    """data/exp_performance_small/summary.csv heuristic rows (config/10.yml, seeds 1..5)."""
+    from vmp import exp
+    pub = {r.split(",")[0]: r for r in _summary("exp_performance_small_summary.csv")}
+    cells = [exp.performance_cell(ag, ag, 1.0, small=True) for ag in ("bestfit", "firstfit")]
+    for row in exp.performance_sweep(cells):
+        assert row == pub[row.split(",")[0]], row
+
+
+def test_vm_size_rows_match_published():
+    """data/exp_vm_size/summary.csv heuristic rows: lowuniform / highuniform VM
+    sizes, reward kl (100 000-step kl returns to 4 decimals)."""
+    from vmp import exp
+    pub = _summary("exp_vm_size_summary.csv")
+    expect = [r for r in pub if not r.startswith("ppo,")]
+    cells = [exp.vm_size_cell(ag, seq) for seq in ("lowuniform", "highuniform")
+             for ag in ("firstfit", "bestfit")]
+    assert exp.vm_size_sweep(cells) == expect

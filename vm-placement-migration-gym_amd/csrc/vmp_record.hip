@@ -122,6 +122,25 @@ __global__ __launch_bounds__(256) void k_record(EnvParams p, RecArgs r) {
   c2 = wsum(c2);
   m1 = wsum(m1);
   m2 = wsum(m2);
+  // per-step variance over PMs, two-pass as np.var (the PM rows are L2-hot);
+  // the cross-env product for exp_performance's variance over seeds reads the
+  // other envs' post-step memory rows (all envs have stepped before this launch)
+  const double cmean = c1 / P, mmean = m1 / P;
+  const bool cross = p.N <= VMP_REC_XMAX;
+  double cv = 0.0, mv = 0.0, xm = 0.0;
+  for (int i = lane; i < P; i += 64) {
+    const double dc = pm[i] - cmean, dm = pm[P + i] - mmean;
+    cv += dc * dc;
+    mv += dm * dm;
+    if (cross) {
+      double col = 0.0;
+      for (int s = 0; s < p.N; s++) col += p.pm[(int64_t)s * 2 * P + P + i];
+      xm += pm[P + i] * col;
+    }
+  }
+  cv = wsum(cv);
+  mv = wsum(mv);
+  xm = wsum(xm);
   sc = wsum(sc);
   sm = wsum(sm);
   life_sum = wsum(life_sum);
@@ -141,6 +160,9 @@ __global__ __launch_bounds__(256) void k_record(EnvParams p, RecArgs r) {
     s[VMP_REC_MEM] += m1;
     s[VMP_REC_MEM2] += m2;
     s[VMP_REC_RANK] += rank;
+    s[VMP_REC_CPUVAR] += cv / P;
+    s[VMP_REC_MEMVAR] += mv / P;
+    s[VMP_REC_XMEM] += xm;
     s[VMP_REC_DROP] += h.total_requests ? (double)h.dropped / (double)h.total_requests : 0.0;
     s[VMP_REC_TCM] += tcm;
     s[VMP_REC_TMM] += tmm;

@@ -93,7 +93,7 @@ def lib():
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 3:
+    if L.vmp_abi_version() != 4:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

@@ -21,7 +21,7 @@ from .config import Config
 
 N_COUNTERS = 6  # total_requests, served, suspend, place, dropped, timestep
 N_STATS = 5     # waiting_ratio, target_cpu_mean, target_mem_mean, total_cpu_req, total_mem_req
-N_REC = 16      # VMP_NREC: recorder sums (include/vmp.h VMP_REC_*)
+N_REC = 19      # VMP_NREC: recorder sums (include/vmp.h VMP_REC_*)
 REC_BINS = 1001
 
 

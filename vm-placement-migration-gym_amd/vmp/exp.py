@@ -7,6 +7,9 @@ comes back to the host. This replaces the reference's process fan-out
 
     python -m vmp.exp suspension --out data.csv            # heuristic rows
     python -m vmp.exp suspension --agents ppo --weights w.pt --out ppo.csv
+    python -m vmp.exp performance --loads 1.0,0.6          # exp_performance.py summary
+    python -m vmp.exp performance_small                    # exp_performance_small.py
+    python -m vmp.exp vm_size                              # exp_vm_size.py summary
 
 Rows are printed in exp_suspension.py's CSV layout (exp_suspension.py:51-58):
 Agent, Load, Service Length, Total Served, Valid Suspend Actions, Valid
@@ -26,7 +29,7 @@ SUSPENSION_HEADER = ("Agent, Load, Service Length, Total Served, Valid Suspend A
 
 # config/100.yml's environment section (the sweeps override reward / arrival rate)
 ENV100 = dict(pms=100, vms=300, service_length=1000, arrival_rate=1.8182, training_steps=10000,
-              eval_steps=100000, seed=0, reward_function="wr", cap_target_util=True,
+              eval_steps=100000, seed=0, reward_function="kl", cap_target_util=True,
               sequence="uniform", beta=0.5, allow_null_action=True)
 PPO100 = dict(episodes=100, hidden_size=512, masked=True, batch_size=100, minibatch_size=25,
               migration_ratio=0.002)
@@ -39,6 +42,9 @@ class Cell:
     service_length: int
     seeds: tuple = (0,)
     weights: str = None
+    cfg: dict = None   # the cell's environment config (else make_config(load, length))
+    ppo: dict = None   # PPOConfig overrides (exp_performance.py:28-33)
+    name: str = None   # row label (jobname)
 
 
 def suspension_config(load, sr, env=ENV100):
@@ -50,12 +56,14 @@ def suspension_config(load, sr, env=ENV100):
     return c
 
 
-def run_cells(cells, make_config, eval_steps=None, chunk=2000, device="cuda:0"):
-    """Evaluate every cell (Base.test per seed, base.py:63-118) for eval_steps and
-    return one list of Record summaries per cell (one dict per seed)."""
-    envs, agents, streams = [], [], []
+def run_cells(cells, make_config=None, eval_steps=None, chunk=2000, device="cuda:0"):
+    """Evaluate every cell (Base.test per seed, base.py:63-118) for its eval_steps
+    and return one list of Record summaries per cell (one dict per seed). All
+    seeds of a cell are the envs of one handle, so the recorder's cross-env sums
+    (VMP_REC_XMEM) span exactly the cell's seeds."""
+    envs, agents, streams, steps = [], [], [], []
     for cell in cells:
-        cfg = make_config(cell.load, cell.service_length)
+        cfg = dict(cell.cfg) if cell.cfg is not None else make_config(cell.load, cell.service_length)
         if eval_steps is not None:
             cfg["eval_steps"] = int(eval_steps)
         s = torch.cuda.Stream(device=device)
@@ -68,25 +76,29 @@ def run_cells(cells, make_config, eval_steps=None, chunk=2000, device="cuda:0"):
             agent = None
             if cell.agent == "ppo":
                 from .ppo import ActStepGraph, PPOAgent, PPOConfig
-                ag = PPOAgent(env, PPOConfig(**PPO100))
+                ag = PPOAgent(env, PPOConfig(**dict(PPO100, **(cell.ppo or {}))))
                 ag.load_model(cell.weights)
                 ag.eval(True)
                 agent = ActStepGraph(ag, warmup=0)
+            elif cell.agent not in ("firstfit", "bestfit"):
+                raise ValueError(f"agent {cell.agent!r} has no batched GPU path")
         envs.append(env)
         agents.append(agent)
         streams.append(s)
-    T = int(eval_steps if eval_steps is not None else make_config(1.0, 1000)["eval_steps"])
-    done = 0
-    while done < T:
-        k = min(chunk, T - done)
-        for cell, env, agent, s in zip(cells, envs, agents, streams):
+        steps.append(int(cfg["eval_steps"]))
+    done = [0] * len(cells)
+    while any(d < t for d, t in zip(done, steps)):
+        for i, (cell, env, agent, s) in enumerate(zip(cells, envs, agents, streams)):
+            k = min(chunk, steps[i] - done[i])
+            if k <= 0:
+                continue
             with torch.cuda.stream(s):
                 if agent is None:
                     env.rollout(cell.agent, k)
                 else:
                     for _ in range(k):
                         agent.replay()
-        done += k
+            done[i] += k
     out = []
     for env, s in zip(envs, streams):
         with torch.cuda.stream(s):
@@ -121,23 +133,136 @@ def suspension_sweep(agents=("firstfit", "bestfit"), loads=None, lengths=None, s
     return [suspension_row(c, r) for c, r in zip(cells, res)]
 
 
+# ------------------------------------------------------------ exp_performance
+PERFORMANCE_HEADER = ("Agent, Load, Return, Drop Rate, Served VM, Suspend Actions, CPU Mean, "
+                      "CPU Variance, Memory Mean, Memory Variance, Pending Rate, Waiting Ratio, "
+                      "Slowdown Rate")
+# config/10.yml's environment section (exp_performance_small.py:20)
+ENV10 = dict(pms=10, vms=30, service_length=1000, arrival_rate=0.0182, training_steps=10000,
+             eval_steps=100000, seed=1, reward_function="kl", cap_target_util=True,
+             sequence="uniform", beta=0.5, allow_null_action=True)
+
+
+def performance_config(load, reward="ut", env=ENV100, jobname=""):
+    """exp_performance.py:20-33: the reward override, arrival_rate =
+    round(pms / 0.55 / service_length * load, 4), and the -masked / -unmasked
+    job suffixes (allow_null_action; the PPO mask follows via Cell.ppo)."""
+    c = dict(env)
+    c.update(reward_function=reward,
+             arrival_rate=float(np.round(c["pms"] / 0.55 / c["service_length"] * load, 4)))
+    if "-masked" in jobname:
+        c["allow_null_action"] = True
+    if "-unmasked" in jobname:
+        c["allow_null_action"] = False
+    return c
+
+
+def performance_cell(agent, jobname, load, reward="ut", weights=None, small=False, seeds=None):
+    """One evaluate() call of exp_performance.py (seeds 0..4) or
+    exp_performance_small.py (config/10.yml, seeds 1..5)."""
+    env = ENV10 if small else ENV100
+    if seeds is None:
+        seeds = tuple(range(1, 6)) if small else tuple(range(5))
+    ppo = None
+    if "-masked" in jobname:
+        ppo = {"masked": True}
+    if "-unmasked" in jobname:
+        ppo = {"masked": False}
+    return Cell(agent, float(load), env["service_length"], tuple(seeds), weights,
+                cfg=performance_config(load, reward, env, jobname), ppo=ppo, name=jobname)
+
+
+def performance_row(cell, summaries):
+    """exp_performance.py:94-138 for one cell from its seeds' device summaries.
+    Memory Variance keeps the reference's axis: np.var(memory, axis=0) is the
+    variance over the seeds per (step, PM), = mean_s E[x^2] - E[(mean_s x)^2],
+    the second term from the recorder's cross-env sums."""
+    f = lambda k: float(np.mean([s[k] for s in summaries]))  # noqa: E731
+    S = len(summaries)
+    mem_var = f("_mem2") - sum(s["_xmem"] for s in summaries) / (S * S)
+    return "%s,%.2f,%.3f,%.3f,%d,%d,%.3f,%.3f,%.3f,%.3f,%.3f,%.3f,%.3f" % (
+        cell.name or cell.agent, cell.load, f("_return"), f("_drop_rate"), f("total served VMs"),
+        f("total suspend actions"), f("_cpu_mean"), f("_cpu_var"), f("_mem_mean"), mem_var,
+        f("_mean_pending"), f("_waiting"), f("_mean_slowdown"))
+
+
+def performance_sweep(cells, eval_steps=None):
+    res = run_cells(cells, eval_steps=eval_steps)
+    return [performance_row(c, r) for c, r in zip(cells, res)]
+
+
+# ---------------------------------------------------------------- exp_vm_size
+VM_SIZE_HEADER = ("Model, Return, Drop Rate, Served VM, Suspend Actions, CPU Mean, "
+                  "CPU Variance, Memory Mean, Memory Variance, Waiting Ratio")
+
+
+def vm_size_config(seq, env=ENV100):
+    """exp_vm_size.py:12-19: config/100.yml (reward kl) with the sequence and an
+    unrounded arrival rate pms / mean size / service_length."""
+    c = dict(env)
+    c["sequence"] = seq
+    if seq == "lowuniform":
+        c["arrival_rate"] = c["pms"] / 0.375 / c["service_length"]
+    elif seq == "highuniform":
+        c["arrival_rate"] = c["pms"] / 0.625 / c["service_length"]
+    return c
+
+
+def vm_size_cell(agent, seq, weights=None, seeds=tuple(range(5))):
+    return Cell(agent, 1.0, ENV100["service_length"], tuple(seeds), weights,
+                cfg=vm_size_config(seq), name=agent)
+
+
+def vm_size_row(cell, summaries):
+    """exp_vm_size.py:60-98 (variances over PMs for both resources)."""
+    f = lambda k: float(np.mean([s[k] for s in summaries]))  # noqa: E731
+    return "%s,%.4f,%.4f,%d,%d,%.4f,%.4f,%.4f,%.4f,%.4f" % (
+        cell.name or cell.agent, f("_return"), f("_drop_rate"), f("total served VMs"),
+        f("total suspend actions"), f("_cpu_mean"), f("_cpu_var"), f("_mem_mean"),
+        f("_mem_var"), f("_waiting"))
+
+
+def vm_size_sweep(cells, eval_steps=None):
+    res = run_cells(cells, eval_steps=eval_steps)
+    return [vm_size_row(c, r) for c, r in zip(cells, res)]
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("experiment", choices=["suspension"])
+    ap.add_argument("experiment", choices=["suspension", "performance", "performance_small",
+                                           "vm_size"])
     ap.add_argument("--agents", default="firstfit,bestfit")
     ap.add_argument("--weights", default=None, help="PPO weights (.pt) for agent ppo")
-    ap.add_argument("--seeds", default="0")
+    ap.add_argument("--seeds", default=None, help="comma list (default: the driver's seeds)")
     ap.add_argument("--loads", default=None, help="comma list (default: the reference grid)")
     ap.add_argument("--lengths", default=None, help="comma list of service lengths")
+    ap.add_argument("--reward", default="ut", help="performance: reward function")
     ap.add_argument("--eval-steps", type=int, default=None)
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
-    rows = suspension_sweep(
-        agents=a.agents.split(","),
-        loads=None if a.loads is None else [float(x) for x in a.loads.split(",")],
-        lengths=None if a.lengths is None else [int(x) for x in a.lengths.split(",")],
-        seeds=[int(x) for x in a.seeds.split(",")], weights=a.weights, eval_steps=a.eval_steps)
-    text = SUSPENSION_HEADER + "\n" + "\n".join(rows) + "\n"
+    agents = a.agents.split(",")
+    seeds = None if a.seeds is None else [int(x) for x in a.seeds.split(",")]
+    loads = None if a.loads is None else [float(x) for x in a.loads.split(",")]
+    if a.experiment == "suspension":
+        header = SUSPENSION_HEADER
+        rows = suspension_sweep(
+            agents=agents, loads=loads,
+            lengths=None if a.lengths is None else [int(x) for x in a.lengths.split(",")],
+            seeds=seeds or [0], weights=a.weights, eval_steps=a.eval_steps)
+    elif a.experiment in ("performance", "performance_small"):
+        header = PERFORMANCE_HEADER
+        small = a.experiment == "performance_small"
+        cells = [performance_cell(ag, "ppo-" + a.reward if ag == "ppo" else ag, ld, a.reward,
+                                  a.weights if ag == "ppo" else None, small, seeds)
+                 for ld in (loads or [1.0]) for ag in agents]
+        rows = performance_sweep(cells, eval_steps=a.eval_steps)
+    else:
+        header = VM_SIZE_HEADER
+        cells = [vm_size_cell(ag, seq, a.weights if ag == "ppo" else None,
+                              tuple(seeds) if seeds else tuple(range(5)))
+                 for seq in ("lowuniform", "highuniform") for ag in agents]
+        rows = vm_size_sweep(cells, eval_steps=a.eval_steps)
+    text = header + "\n" + "\n".join(rows) + "\n"
     if a.out:
         with open(a.out, "w") as f:
             f.write(text)

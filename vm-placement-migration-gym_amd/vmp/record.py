@@ -164,6 +164,7 @@ class NpEncoder(json.JSONEncoder):
 REC_STEPS, REC_REWARD, REC_CPU, REC_CPU2, REC_MEM, REC_MEM2, REC_RANK, REC_DROP = range(8)
 REC_TCM, REC_TMM, REC_WAITING, REC_LIFE_SUM, REC_LIVES, REC_REWARD_OK, REC_N_OK, REC_N_BAD = \
     range(8, 16)
+REC_CPUVAR, REC_MEMVAR, REC_XMEM = range(16, 19)
 
 
 def _hist_stats(h):
@@ -220,4 +221,14 @@ def summary_from_device(hist, sums, counters, stats, pms):
         "_mean_pending": pend[0] if pend else np.nan,
         "_mean_slowdown": slow[0],
         "_max_slowdown": slow[2],
+        # per-step series means the exp_performance / exp_vm_size summaries print
+        "_return": np.round(total, 3),
+        "_drop_rate": sums[REC_DROP] / T,
+        "_cpu_mean": cm,
+        "_mem_mean": mm,
+        "_cpu_var": sums[REC_CPUVAR] / T,
+        "_mem_var": sums[REC_MEMVAR] / T,
+        "_waiting": sums[REC_WAITING] / T,
+        "_mem2": sums[REC_MEM2] / TP,
+        "_xmem": sums[REC_XMEM] / TP,
     }
