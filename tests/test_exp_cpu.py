@@ -44,3 +44,14 @@ def test_experiment_configs():
     assert exp.performance_cell("firstfit", "firstfit", 1.0, small=True).seeds == (1, 2, 3, 4, 5)
     v = exp.vm_size_config("highuniform")
     assert v["arrival_rate"] == 100 / 0.625 / 1000 and v["reward_function"] == "kl"
+
+
+def test_reward_and_migration_rows():
+    rng = np.random.default_rng(4)
+    cpu, mem = rng.random((3, 20, 10)), rng.random((3, 20, 10))
+    cell = exp.reward_cell("ppo", "kl", "w.pt")
+    row = exp.reward_row(cell, _summaries(cpu, mem)).split(",")
+    assert row[:2] == ["ppo", "kl"] and cell.cfg["arrival_rate"] == 0.182
+    assert float(row[9]) == float("%.3f" % np.mean(np.mean(np.var(mem, axis=2), axis=0)))
+    m = exp.migration_cell("bestfit", "ut", 0.003)
+    assert exp.migration_row(m, _summaries(cpu, mem)) == "bestfit,ut,0.003,%.3f,0.000" % cpu[0].mean()

@@ -85,3 +85,26 @@ def test_vm_size_rows_match_published():
     cells = [exp.vm_size_cell(ag, seq) for seq in ("lowuniform", "highuniform")
              for ag in ("firstfit", "bestfit")]
     assert exp.vm_size_sweep(cells) == expect
+
+
+def test_migration_ratio_bestfit_rows_match_published():
+    """data/exp_migration_ratio/data.csv bestfit rows (config/100.yml seed 0,
+    100 000 steps; BestFit ignores the ratio)."""
+    from vmp import exp
+    with open(os.path.join(GOLDEN, "exp_migration_ratio_data.csv")) as f:
+        pub = {r.strip() for r in f if r.startswith("bestfit,")}
+    cells = [exp.migration_cell("bestfit", "ut", r) for r in (0.0, 0.001)]
+    rows = exp.migration_sweep(cells)
+    assert rows[0] == "bestfit,ut,0.000,0.761,0.000" and set(rows) <= pub, rows
+
+
+def test_exp_cli(tmp_path, capsys):
+    """python -m vmp.exp <experiment>: header plus one row per cell, to --out."""
+    from vmp import exp
+    out = tmp_path / "m.csv"
+    exp.main(["migration_ratio", "--agents", "bestfit", "--eval-steps", "200", "--out", str(out)])
+    lines = out.read_text().splitlines()
+    assert lines[0] == exp.MIGRATION_HEADER and len(lines) == 11
+    exp.main(["performance", "--loads", "1.0,0.6", "--eval-steps", "200"])
+    lines = capsys.readouterr().out.splitlines()
+    assert lines[-5] == exp.PERFORMANCE_HEADER and len(lines[-4:]) == 4

@@ -10,6 +10,8 @@ comes back to the host. This replaces the reference's process fan-out
     python -m vmp.exp performance --loads 1.0,0.6          # exp_performance.py summary
     python -m vmp.exp performance_small                    # exp_performance_small.py
     python -m vmp.exp vm_size                              # exp_vm_size.py summary
+    python -m vmp.exp reward --agents ppo --weights 'w/ppo-{reward}.pt'   # exp_reward.py
+    python -m vmp.exp migration_ratio --agents bestfit,ppo --weights 'w/ppo-{reward}.pt'
 
 Rows are printed in exp_suspension.py's CSV layout (exp_suspension.py:51-58):
 Agent, Load, Service Length, Total Served, Valid Suspend Actions, Valid
@@ -227,16 +229,73 @@ def vm_size_sweep(cells, eval_steps=None):
     return [vm_size_row(c, r) for c, r in zip(cells, res)]
 
 
+# ------------------------------------------------------ exp_reward / migration
+REWARD_HEADER = ("Agent, Reward, Return, Drop Rate, Served VM, Suspend Actions, CPU Mean, "
+                 "CPU Variance, Memory Mean, Memory Variance, Pending Rate, Waiting Ratio, "
+                 "Slowdown Rate")
+MIGRATION_HEADER = "Agent,Reward,Migration Ratio,CPU,Average Slowdown"
+
+
+def reward_config(reward, env=ENV100):
+    """exp_reward.py:24-28 / exp_migration_ratio.py:13-16: the reward, uniform
+    sizes, arrival_rate = round(pms / 0.55 / service_length, 3)."""
+    c = dict(env)
+    c.update(reward_function=reward, sequence="uniform",
+             arrival_rate=float(np.round(c["pms"] / 0.55 / c["service_length"], 3)))
+    return c
+
+
+def reward_cell(agent, reward, weights=None, migration_ratio=0.002, seeds=tuple(range(5))):
+    """One evaluate_seeds() call of exp_reward.py (seeds 0..4)."""
+    return Cell(agent, 1.0, ENV100["service_length"], tuple(seeds), weights,
+                cfg=reward_config(reward), ppo={"migration_ratio": migration_ratio},
+                name=agent)
+
+
+def reward_row(cell, summaries):
+    """exp_reward.py:108-135 (variances over PMs for both resources)."""
+    f = lambda k: float(np.mean([s[k] for s in summaries]))  # noqa: E731
+    return "%s,%s,%.3f,%.3f,%d,%d,%.3f,%.3f,%.3f,%.3f,%.3f,%.3f,%.3f" % (
+        cell.name or cell.agent, cell.cfg["reward_function"], f("_return"), f("_drop_rate"),
+        f("total served VMs"), f("total suspend actions"), f("_cpu_mean"), f("_cpu_var"),
+        f("_mem_mean"), f("_mem_var"), f("_mean_pending"), f("_waiting"), f("_mean_slowdown"))
+
+
+def reward_sweep(cells, eval_steps=None):
+    res = run_cells(cells, eval_steps=eval_steps)
+    return [reward_row(c, r) for c, r in zip(cells, res)]
+
+
+def migration_cell(agent, reward, migration_ratio, weights=None):
+    """One evaluate() call of exp_migration_ratio.py (config seed 0, one run)."""
+    return Cell(agent, 1.0, ENV100["service_length"], (0,), weights, cfg=reward_config(reward),
+                ppo={"migration_ratio": float(migration_ratio)}, name=agent)
+
+
+def migration_row(cell, summaries):
+    """exp_migration_ratio.py:43-48: mean CPU and mean slowdown of the one run."""
+    s = summaries[0]
+    return "%s,%s,%.3f,%.3f,%.3f" % (cell.name or cell.agent, cell.cfg["reward_function"],
+                                     cell.ppo["migration_ratio"], s["_cpu_mean"],
+                                     s["_mean_slowdown"])
+
+
+def migration_sweep(cells, eval_steps=None):
+    res = run_cells(cells, eval_steps=eval_steps)
+    return [migration_row(c, r) for c, r in zip(cells, res)]
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("experiment", choices=["suspension", "performance", "performance_small",
-                                           "vm_size"])
+                                           "vm_size", "reward", "migration_ratio"])
     ap.add_argument("--agents", default="firstfit,bestfit")
     ap.add_argument("--weights", default=None, help="PPO weights (.pt) for agent ppo")
     ap.add_argument("--seeds", default=None, help="comma list (default: the driver's seeds)")
     ap.add_argument("--loads", default=None, help="comma list (default: the reference grid)")
     ap.add_argument("--lengths", default=None, help="comma list of service lengths")
-    ap.add_argument("--reward", default="ut", help="performance: reward function")
+    ap.add_argument("--reward", default=None,
+                    help="reward function(s): performance (default ut), reward (default wr,ut,kl)")
     ap.add_argument("--eval-steps", type=int, default=None)
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
@@ -252,10 +311,26 @@ def main(argv=None):
     elif a.experiment in ("performance", "performance_small"):
         header = PERFORMANCE_HEADER
         small = a.experiment == "performance_small"
-        cells = [performance_cell(ag, "ppo-" + a.reward if ag == "ppo" else ag, ld, a.reward,
+        reward = a.reward or "ut"
+        cells = [performance_cell(ag, "ppo-" + reward if ag == "ppo" else ag, ld, reward,
                                   a.weights if ag == "ppo" else None, small, seeds)
                  for ld in (loads or [1.0]) for ag in agents]
         rows = performance_sweep(cells, eval_steps=a.eval_steps)
+    elif a.experiment == "reward":
+        header = REWARD_HEADER
+        rewards = a.reward.split(",") if a.reward else ["wr", "ut", "kl"]
+        cells = [reward_cell(ag, rw, a.weights.replace("{reward}", rw) if ag == "ppo" else None,
+                             seeds=tuple(seeds) if seeds else tuple(range(5)))
+                 for ag in agents for rw in rewards]
+        rows = reward_sweep(cells, eval_steps=a.eval_steps)
+    elif a.experiment == "migration_ratio":
+        header = MIGRATION_HEADER
+        ratios = [round(0.001 * i, 3) for i in range(10)]
+        cells = [migration_cell(ag, rw, r, a.weights.replace("{reward}", rw)
+                                if ag == "ppo" else None)
+                 for r in ratios for ag in agents
+                 for rw in (["ut"] if ag != "ppo" else ["wr", "ut", "kl"])]
+        rows = migration_sweep(cells, eval_steps=a.eval_steps)
     else:
         header = VM_SIZE_HEADER
         cells = [vm_size_cell(ag, seq, a.weights if ag == "ppo" else None,
