@@ -108,3 +108,16 @@ def test_exp_cli(tmp_path, capsys):
     exp.main(["performance", "--loads", "1.0,0.6", "--eval-steps", "200"])
     lines = capsys.readouterr().out.splitlines()
     assert lines[-5] == exp.PERFORMANCE_HEADER and len(lines[-4:]) == 4
+
+
+def test_graph_recorded_rollout_equals_plain_launches():
+    """The captured recorded rollout (graph_steps) gives the same Record
+    summaries as one launch pair per step, including a remainder."""
+    from vmp import exp
+    cells = [exp.performance_cell("bestfit", "bestfit", 1.0, "kl", seeds=(0, 1, 2))]
+    a = exp.run_cells(cells, eval_steps=1234, graph_steps=100)[0]
+    b = exp.run_cells(cells, eval_steps=1234, graph_steps=0)[0]
+    for x, y in zip(a, b):
+        assert x.keys() == y.keys()
+        for key in x:
+            assert (x[key] == y[key]) or (x[key] != x[key] and y[key] != y[key]), key

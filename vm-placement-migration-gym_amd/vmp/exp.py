@@ -58,11 +58,34 @@ def suspension_config(load, sr, env=ENV100):
     return c
 
 
-def run_cells(cells, make_config=None, eval_steps=None, chunk=2000, device="cuda:0"):
+class _RecordedRollout:
+    """`g_steps` recorded heuristic steps (act+step, then the recorder: two
+    launches per step) of one env captured as a HIP graph, so a long eval costs
+    one graph launch per g_steps steps instead of 2 * g_steps kernel launches."""
+
+    def __init__(self, env, policy, g_steps):
+        self.env, self.policy, self.g = env, policy, g_steps
+        n = env.n_envs
+        self.rew = torch.empty((g_steps, n), dtype=torch.float64, device=env.device)
+        self.dc = torch.zeros(n, dtype=torch.int64, device=env.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            env.rollout(policy, g_steps, rewards=self.rew, done_count=self.dc)
+
+    def run(self, k):
+        for _ in range(k // self.g):
+            self.graph.replay()
+        if k % self.g:
+            self.env.rollout(self.policy, k % self.g)
+
+
+def run_cells(cells, make_config=None, eval_steps=None, chunk=2000, device="cuda:0",
+              graph_steps=100):
     """Evaluate every cell (Base.test per seed, base.py:63-118) for its eval_steps
     and return one list of Record summaries per cell (one dict per seed). All
     seeds of a cell are the envs of one handle, so the recorder's cross-env sums
-    (VMP_REC_XMEM) span exactly the cell's seeds."""
+    (VMP_REC_XMEM) span exactly the cell's seeds. Heuristic cells replay a
+    captured graph of graph_steps recorded steps (0 = plain launches)."""
     envs, agents, streams, steps = [], [], [], []
     for cell in cells:
         cfg = dict(cell.cfg) if cell.cfg is not None else make_config(cell.load, cell.service_length)
@@ -84,6 +107,8 @@ def run_cells(cells, make_config=None, eval_steps=None, chunk=2000, device="cuda
                 agent = ActStepGraph(ag, warmup=0)
             elif cell.agent not in ("firstfit", "bestfit"):
                 raise ValueError(f"agent {cell.agent!r} has no batched GPU path")
+            elif graph_steps:
+                agent = _RecordedRollout(env, cell.agent, int(graph_steps))
         envs.append(env)
         agents.append(agent)
         streams.append(s)
@@ -97,6 +122,8 @@ def run_cells(cells, make_config=None, eval_steps=None, chunk=2000, device="cuda
             with torch.cuda.stream(s):
                 if agent is None:
                     env.rollout(cell.agent, k)
+                elif isinstance(agent, _RecordedRollout):
+                    agent.run(k)
                 else:
                     for _ in range(k):
                         agent.replay()
