@@ -188,16 +188,18 @@ void carve(vmp_handle *h) {
     const int64_t bits = 2 * 101 * 8 * (int64_t)p.NW, acc = 4 * V;
     off = align16(off + (bits > acc ? bits : acc));
   }
-  p.off_sort = (int32_t)off;
-  off = align16(off + 4 * 256);          // introsort stacks (BF)
   p.off_stage = (int32_t)off;
   off = align16(off + 8 * 16);           // reduction results + draw bookkeeping
+  // ccomp, mcomp u8 (stats, after the action phase) share their region with
+  // the BF introsort stacks (action phase only)
   p.off_ccomp = (int32_t)off;
-  off = align16(off + 2 * V);            // ccomp, mcomp u8
+  p.off_sort = (int32_t)off;
+  off = align16(off + (2 * V > 4 * 256 ? 2 * V : 4 * 256));
+  // the LDS plan of the pairwise sums exists only for n > 1928 (wave_pw_sum)
   p.off_leaf = (int32_t)off;
-  off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);  // lo, len, lane-0 stack
+  if (deep) off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);  // lo, len, lane-0 stack
   p.off_leafval = (int32_t)off;
-  off = align16(off + 8 * 8 * (int64_t)p.n_leaf + 8 * (2 * (int64_t)p.n_leaf + 64));
+  if (deep) off = align16(off + 8 * 8 * (int64_t)p.n_leaf + 8 * (2 * (int64_t)p.n_leaf + 64));
   p.off_pre = (int32_t)off;   // per-launch random draws follow (launch_env)
   p.lds_wave_bytes = (int32_t)off;
 }
