@@ -191,10 +191,10 @@ void carve(vmp_handle *h) {
   p.off_stage = (int32_t)off;
   off = align16(off + 8 * 16);           // reduction results + draw bookkeeping
   // ccomp, mcomp u8 (stats, after the action phase) share their region with
-  // the BF introsort stacks (action phase only)
+  // the BF introsort stacks + partition lists (action phase only)
   p.off_ccomp = (int32_t)off;
   p.off_sort = (int32_t)off;
-  off = align16(off + (2 * V > 4 * 256 ? 2 * V : 4 * 256));
+  off = align16(off + (2 * V > 4 * 256 + 4 * P ? 2 * V : 4 * 256 + 4 * P));
   // the LDS plan of the pairwise sums exists only for n > 1928 (wave_pw_sum)
   p.off_leaf = (int32_t)off;
   if (deep) off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);  // lo, len, lane-0 stack

@@ -468,8 +468,13 @@ __device__ void aheapsort_lds(const float LDSP *v, uint16_t LDSP *tosort, int n)
   }
 }
 
+// Only the sorted positions lo..hi are needed (BF's tie block): numpy sorts
+// every partition independently of the others, so a partition that does not
+// intersect [lo, hi] is dropped instead of sorted, and positions lo..hi come
+// out exactly as the full sort leaves them (a quickselect-shaped walk:
+// ~2n element visits instead of ~n log n).
 __device__ __noinline__ void aquicksort_lds(const float LDSP *v, uint16_t LDSP *t, int num,
-                                            int32_t LDSP *stack) {
+                                            int32_t LDSP *stack, int lo, int hi) {
   int32_t LDSP *depth = stack + 128;
   int pl = 0, pr = num - 1;
   int sp = 0, dp = 0;
@@ -477,6 +482,7 @@ __device__ __noinline__ void aquicksort_lds(const float LDSP *v, uint16_t LDSP *
   for (int u = num; u >>= 1;) cdepth++;
   cdepth *= 2;
   for (;;) {
+    if (pr < lo || pl > hi) goto stack_pop;
     if (cdepth < 0) {
       aheapsort_lds(v, t + pl, pr - pl + 1);
       goto stack_pop;
@@ -508,6 +514,7 @@ __device__ __noinline__ void aquicksort_lds(const float LDSP *v, uint16_t LDSP *
         pl = pi + 1;
       }
       depth[dp++] = --cdepth;
+      if (pr < lo || pl > hi) goto stack_pop;
     }
     for (int pi = pl + 1; pi <= pr; ++pi) {
       uint16_t vi = t[pi];
@@ -522,6 +529,153 @@ __device__ __noinline__ void aquicksort_lds(const float LDSP *v, uint16_t LDSP *
     pl = stack[--sp];
     cdepth = depth[--dp];
   }
+}
+
+// Wave-parallel form of the same sort (all 64 lanes, uniform control flow),
+// identical result. numpy's partition loop
+//   do ++pi while v[pi] < vp;  do --pj while vp < v[pj];  if (pi >= pj) break;  swap
+// pairs the k-th left stop A[k] (ascending positions in (pl, pr-1] with
+// v >= vp; pr-1 holds the pivot) with the k-th right stop B[k] (descending
+// positions in [pl, pr-2] with v <= vp; pl holds a value <= vp) while
+// A[k] < B[k]: up to that point each scan only crosses unmodified positions,
+// so both lists follow from the values before the loop. With K = #{k : A[k] <
+// B[k]} (a prefix, A rising and B falling), the K swaps are disjoint, and the
+// final left stop is min(A[K], B[K-1]) (B[K-1] holds a swapped-in value >= vp).
+// Stops are ranked with ballots; the lists live in `scr` (u16, 2 x n). Small
+// partitions (<= 16) get numpy's insertion sort as a stable rank sort; the
+// depth-limit heapsort stays on lane 0.
+__device__ __noinline__ void wave_aquicksort(const float LDSP *v, uint16_t LDSP *t, int num,
+                                             int32_t LDSP *stack, int lo, int hi,
+                                             uint16_t LDSP *scr) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int32_t LDSP *depth = stack + 128;
+  int pl = 0, pr = num - 1;
+  int sp = 0, dp = 0;
+  int cdepth = 0;
+  for (int u = num; u >>= 1;) cdepth++;
+  cdepth *= 2;
+  for (;;) {
+    if (pr < lo || pl > hi) goto stack_pop;
+    if (cdepth < 0) {
+      if (lane == 0) aheapsort_lds(v, t + pl, pr - pl + 1);
+      wsync();
+      goto stack_pop;
+    }
+    while ((pr - pl) > 15) {
+      const int pm = pl + ((pr - pl) >> 1);
+      uint16_t tl = t[pl], tm = t[pm], tr = t[pr], x;
+      if (fless(v[tm], v[tl])) { x = tm; tm = tl; tl = x; }
+      if (fless(v[tr], v[tm])) { x = tr; tr = tm; tm = x; }
+      if (fless(v[tm], v[tl])) { x = tm; tm = tl; tl = x; }
+      const float vp = v[tm];
+      const uint16_t tq = t[pr - 1];
+      wsync();
+      if (lane == 0) {
+        t[pl] = tl;
+        t[pm] = tq;
+        t[pr] = tr;
+        t[pr - 1] = tm;
+      }
+      wsync();
+      uint16_t LDSP *apos = scr;
+      uint16_t LDSP *bpos = scr + (pr - pl + 1);
+      int nb = 0;  // B: descending from pr-2
+      for (int c = pr - 2; c >= pl; c -= 64) {
+        const int q = c - lane;
+        const bool f = q >= pl && !fless(vp, v[t[q]]);
+        const uint64_t m = ballot(f);
+        if (f) bpos[nb + __popcll(m & lt)] = (uint16_t)q;
+        nb += __popcll(m);
+      }
+      int na = 0;  // A: ascending from pl+1
+      for (int c = pl + 1; c <= pr - 1; c += 64) {
+        const int q = c + lane;
+        const bool f = q <= pr - 1 && !fless(v[t[q]], vp);
+        const uint64_t m = ballot(f);
+        if (f) apos[na + __popcll(m & lt)] = (uint16_t)q;
+        na += __popcll(m);
+      }
+      wsync();
+      int kk = 0;  // K: A[k] < B[k] holds for a prefix of k
+      for (int c = 0; c < na && c < nb; c += 64) {
+        const int k = c + lane;
+        const bool sw = k < na && k < nb && (int)apos[k] < (int)bpos[k];
+        kk += __popcll(ballot(sw));
+      }
+      for (int c = 0; c < kk; c += 64) {
+        const int k = c + lane;
+        uint16_t xa = 0, xb = 0;
+        int qa = 0, qb = 0;
+        if (k < kk) {
+          qa = apos[k];
+          qb = bpos[k];
+          xa = t[qa];
+          xb = t[qb];
+        }
+        wsync();
+        if (k < kk) {
+          t[qa] = xb;
+          t[qb] = xa;
+        }
+        wsync();
+      }
+      int pi = apos[kk];
+      if (kk > 0 && (int)bpos[kk - 1] < pi) pi = bpos[kk - 1];
+      wsync();
+      if (lane == 0) {
+        x = t[pi];
+        t[pi] = t[pr - 1];
+        t[pr - 1] = x;
+      }
+      wsync();
+      if (pi - pl < pr - pi) {
+        if (lane == 0) {
+          stack[sp] = pi + 1;
+          stack[sp + 1] = pr;
+        }
+        sp += 2;
+        pr = pi - 1;
+      } else {
+        if (lane == 0) {
+          stack[sp] = pl;
+          stack[sp + 1] = pi - 1;
+        }
+        sp += 2;
+        pl = pi + 1;
+      }
+      --cdepth;
+      if (lane == 0) depth[dp] = cdepth;
+      dp++;
+      wsync();
+      if (pr < lo || pl > hi) goto stack_pop;
+    }
+    {  // insertion sort of [pl, pr] (<= 16 elements) = stable sort by value
+      const int n = pr - pl + 1;
+      uint16_t me = 0;
+      float vm = 0.f;
+      if (lane < n) {
+        me = t[pl + lane];
+        vm = v[me];
+      }
+      int rank = 0;
+      for (int j = 0; j < n; j++) {
+        const float vj = __shfl(vm, j);
+        rank += (fless(vj, vm) || (j < lane && !fless(vm, vj))) ? 1 : 0;
+      }
+      wsync();
+      if (lane < n) t[pl + rank] = me;
+      wsync();
+    }
+  stack_pop:
+    if (sp == 0) break;
+    wsync();
+    sp -= 2;
+    pl = stack[sp];
+    pr = stack[sp + 1];
+    cdepth = depth[--dp];
+  }
+  wsync();
 }
 
 // --------------------------------------------------------- env kernel ----
@@ -712,30 +866,14 @@ __device__ __forceinline__ int bm_query(const Lds &L, int NW, int kc, int km) {
   return -1;
 }
 
-__device__ __forceinline__ void bf_sort(const EnvParams &p, const Lds &L) {
-  const int lane = lane_id();
-  const int P = p.P;
-  for (int i = lane; i < P; i += 64) L.fkey[i] = L.fcpu[i] + L.fmem[i];
-  wsync();
-  if (lane == 0) {
-    for (int i = 0; i < P; i++) L.ord[i] = (uint16_t)i;
-    aquicksort_lds(L.fkey, L.ord, P, L.sortstk);
-    // reverse in place: np.flip(argsort) = visiting order
-    for (int i = 0, j = P - 1; i < j; i++, j--) {
-      uint16_t x = L.ord[i];
-      L.ord[i] = L.ord[j];
-      L.ord[j] = x;
-    }
-  }
-  wsync();
-}
-
 // BestFit's choice for sizes (kc, km) (bestfit.py:33-39): the first PM in
 // visiting order flip(argsort(fcpu + fmem)) that fits, i.e. the fitting PM of
 // largest key. Fast path: a wave argmax over the PMs; only when two or more
-// fitting PMs share the largest key does their order matter, and then the
-// scalar introsort (bf_sort, numpy's tie order) runs and the
-// first fitting visiting position is taken. Returns -1 if nothing fits.
+// fitting PMs share the largest key m does their order matter. The keys equal
+// to m occupy the ascending positions [P - above - eq, P - above) (above =
+// keys > m, none of which fits); the scalar introsort (numpy's tie order,
+// SURVEY App. C) is run for that block only, and its highest fitting position
+// (the first in visiting order) is taken. Returns -1 if nothing fits.
 __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int kc, int km) {
   const int lane = lane_id();
   const int P = p.P;
@@ -764,11 +902,33 @@ __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int k
     const uint64_t who = ballot(best == m && cnt == 1);
     return __builtin_amdgcn_readlane(bi, __ffsll((unsigned long long)who) - 1);
   }
-  bf_sort(p, L);  // ties at the top: numpy's order decides
-  for (int b = 0; b < P; b += 64) {
-    const int i = b + lane;
-    const int q = i < P ? (int)L.ord[i] : 0;
-    const uint64_t f = ballot(i < P && (int)L.tc[q] - 1 >= kc && (int)L.tm[q] - 1 >= km);
+  // ties at the top: numpy's order decides
+  int above = 0, eq = 0;
+  for (int i = lane; i < P; i += 64) {
+    const float key = L.fcpu[i] + L.fmem[i];
+    L.fkey[i] = key;
+    L.ord[i] = (uint16_t)i;
+    above += key > m;
+    eq += key == m;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    above += __shfl_xor(above, o);
+    eq += __shfl_xor(eq, o);
+  }
+  const int hi = P - above - 1, lo = P - above - eq;
+  wsync();
+#ifdef VMP_SERIAL_SORT
+  if (lane == 0) aquicksort_lds(L.fkey, L.ord, P, L.sortstk, lo, hi);
+#else
+  wave_aquicksort(L.fkey, L.ord, P, L.sortstk, lo, hi,
+                  reinterpret_cast<uint16_t LDSP *>(L.sortstk + 256));
+#endif
+  wsync();
+  for (int b = hi; b >= lo; b -= 64) {  // visiting order: descending positions
+    const int pos = b - lane;
+    const int q = pos >= lo ? (int)L.ord[pos] : 0;
+    const uint64_t f = ballot(pos >= lo && (int)L.tc[q] - 1 >= kc && (int)L.tm[q] - 1 >= km);
     if (f) return __builtin_amdgcn_readlane(q, __ffsll((unsigned long long)f) - 1);
   }
   return -1;
