@@ -68,8 +68,13 @@ def main():
         import torch.distributed as dist
         import datetime
         # a rank that fails a leg must not leave the others waiting forever
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local),
-                                timeout=datetime.timedelta(seconds=300))
+        backend = os.environ.get("VMP_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                    timeout=datetime.timedelta(seconds=300))
+        else:  # rehearsal of the N > 1 path with several ranks on one GPU
+            dist.init_process_group(backend, timeout=datetime.timedelta(seconds=300))
+            local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
