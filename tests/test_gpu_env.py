@@ -240,9 +240,12 @@ def test_gae_matches_reference_loop():
 def test_large_v_block_kernel_vs_oracle(policy, reward):
     """V > 1024 runs k_env_big (one workgroup per env): P1000 / V3000 and
     P200 / V10000 (the stress config's slot count) against the C oracle,
-    heuristic act+step and random external actions, bit-exact."""
+    heuristic act+step and random external actions, bit-exact. The third case
+    (2000 arrivals and hundreds of finishers per step at P1000 / V10000) runs
+    the block kernel's > 512-event chunks of the accept and free phases."""
     from vmp.batched import BatchedVmEnv
-    for P, V, lam, L, steps in ((1000, 3000, 9.0, 300, 40), (200, 10000, 30.0, 400, 25)):
+    for P, V, lam, L, steps in ((1000, 3000, 9.0, 300, 40), (200, 10000, 30.0, 400, 25),
+                                (1000, 10000, 2000.0, 2, 8)):
         cfg = dict(pms=P, vms=V, arrival_rate=lam, service_length=L, training_steps=10000,
                    eval_steps=100000, seed=5, reward_function=reward, sequence="uniform",
                    cap_target_util=True, beta=0.5, allow_null_action=True)

@@ -214,6 +214,13 @@ void launch_vpt(int need, dim3 grid, dim3 block, size_t lds, hipStream_t s, cons
   else hipLaunchKernelGGL((k_env<16, ONE>), grid, block, lds, s, p, o);
 }
 
+// k_env_big's shape: the fewest slots per thread that fit 512 threads, and the
+// thread count (whole waves). The block's VM words live in LDS (4 B per slot).
+void big_shape(int64_t V, int &spt, int &nt) {
+  spt = V <= 4 * kBigMaxThreads ? 4 : V <= 8 * kBigMaxThreads ? 8 : V <= 16 * kBigMaxThreads ? 16 : 20;
+  nt = (int)(64 * ((V + 64 * spt - 1) / (64 * spt)));
+}
+
 int launch_env(vmp_handle *h, const StepOut &o) {
   dim3 grid((h->N + kEnvWavesPerBlock - 1) / kEnvWavesPerBlock), block(64 * kEnvWavesPerBlock);
   EnvParams p = h->prm;
@@ -224,12 +231,10 @@ int launch_env(vmp_handle *h, const StepOut &o) {
   size_t lds = (size_t)p.lds_wave_bytes * kEnvWavesPerBlock;
   if (!h->big && lds > 160 * 1024 - 2048) return fail(VMP_EINVAL, "config too large for the LDS carve");
   if (h->big) {
-    // one workgroup per env: the fewest slots per thread that fit 1024 threads
-    const int spt = h->V <= 4 * kBigMaxThreads ? 4
-                    : h->V <= 8 * kBigMaxThreads ? 8
-                    : h->V <= 16 * kBigMaxThreads ? 16 : 20;
-    const int nt = 64 * ((h->V + 64 * spt - 1) / (64 * spt));
-    const size_t lds1 = (size_t)p.lds_wave_bytes;
+    // one workgroup per env; the VM words follow the wave carve
+    int spt, nt;
+    big_shape(h->V, spt, nt);
+    const size_t lds1 = (size_t)p.lds_wave_bytes + 4 * (size_t)spt * nt;
     if (spt == 4) hipLaunchKernelGGL(k_env_big<4>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
     else if (spt == 8) hipLaunchKernelGGL(k_env_big<8>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
     else if (spt == 16) hipLaunchKernelGGL(k_env_big<16>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
@@ -361,7 +366,10 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   }
   {
     const int64_t per_env = p.lds_wave_bytes + 20 * kSpecDraws + 4 * kMaxStepsPerLaunch;
-    const int64_t need = h->big ? per_env + kBigStaticLds : per_env * kEnvWavesPerBlock + 2048;
+    int spt = 0, nt = 0;
+    if (h->big) big_shape(h->V, spt, nt);
+    const int64_t need = h->big ? per_env + kBigStaticLds + 4 * (int64_t)spt * nt
+                                : per_env * kEnvWavesPerBlock + 2048;
     if (need > 160 * 1024) {
       vmp_destroy(h);
       return fail(VMP_EINVAL, "config too large for the LDS carve of this build");

@@ -1945,18 +1945,34 @@ __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, ui
 
 // ------------------------------------------------------- large-V env kernel
 // V > 1024 (e.g. the P1000 / V10000 stress config): one workgroup of NT =
-// 64 * NWV threads per env. Thread t holds VM slots v = s*NT + t (s < SPT) in
-// registers, so slot order (s, t) is ascending VM order. PM-level work (fit
-// bitmaps, BF sort, placements, frees, RNG draws, pairwise sums, reward) runs
-// on wave 0 with the wave kernel's helpers; per-VM events that the reference
-// applies in VM order are compacted across the block (bcx_rank, ascending t
-// within each s) and applied by wave 0 in that order. Same arithmetic, same
+// 64 * NWV threads per env. Thread t owns VM slots v = s*NT + t (s < SPT), so
+// slot order (s, t) is ascending VM order. The VM words live in LDS (W[v]),
+// the remaining service times in registers (rem[s], only touched by fully
+// unrolled loops, so they stay statically indexed: a dynamically indexed
+// register array would live in scratch, which at 512 threads x 500 B per CU
+// misses L2). PM-level work (fit bitmaps, BF sort, placements, frees, RNG
+// draws, pairwise sums, reward) runs on wave 0 with the wave kernel's helpers;
+// per-VM events that the reference applies in VM order are ranked across the
+// block (row_counts + slot_rank: one barrier pair for all SPT slot rows) and
+// applied by wave 0 in that order. Same arithmetic, same
 // order as k_env: the two kernels are interchangeable (VMP_BIG_KERNEL=1
 // forces this one for any V, which the parity tests use).
+// Slot-row loops of the block kernel (s = 0..SPT-1). Rolled: a full unroll
+// (-DVMP_BIG_UNROLL) hoists enough per-slot temporaries to grow the scratch
+// from 496 to 3296 B per lane at SPT = 20.
+#ifdef VMP_BIG_UNROLL
+#define VMP_SLOOP _Pragma("unroll")
+#else
+#define VMP_SLOOP _Pragma("unroll 1")
+#endif
+
+constexpr int kBigMaxSPT = 20, kBigMaxWaves = 8;
 struct BigShared {
   int32_t wcnt[16];   // per-wave counts of a compaction
   int32_t bc[8];      // broadcast scalars
   int64_t b64[4];
+  int32_t rc[kBigMaxSPT * kBigMaxWaves];  // per slot row, per wave flag counts (row_counts)
+  int32_t rtot[kBigMaxWaves];             // per wave flag totals
   uint32_t evw[512];  // event list (one slot row of the block): VM word
   int32_t evt[512];   // event list: target / value
   uint8_t evok[512];  // event results
@@ -1978,6 +1994,44 @@ __device__ __forceinline__ int bcx_rank(bool flag, BigShared &B, int &total) {
   }
   total = tot;
   return off + below(m, lane);
+}
+
+// Flag counts of all SPT slot rows at once (bit s of fl = slot s*NT + t):
+// B.rc[s][wave] and the block total. Two barriers for all rows.
+template <int SPT>
+__device__ __forceinline__ int row_counts(uint32_t fl, BigShared &B) {
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  __syncthreads();
+  int wt = 0;
+#pragma unroll
+  for (int s = 0; s < SPT; s++) {
+    const int c = __popcll(ballot((fl >> s) & 1u));
+    wt += c;
+    if (lane == 0) B.rc[s * kBigMaxWaves + wid] = c;
+  }
+  if (lane == 0) B.rtot[wid] = wt;
+  __syncthreads();
+  int tot = 0;
+  for (int i = 0; i < nwv; i++) tot += B.rtot[i];
+  return tot;
+}
+
+// Rank (ascending VM order) of slot row s of this thread in the flag set
+// counted by row_counts; `base` carries the flags of rows < s (start at 0 and
+// call for s = 0, 1, ... in order). Valid for flagged slots only.
+__device__ __forceinline__ int slot_rank(uint32_t fl, int s, const BigShared &B, int &base) {
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const uint64_t m = ballot((fl >> s) & 1u);
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBigMaxWaves; w++) {  // rows of absent waves stay 0
+    const int c = B.rc[s * kBigMaxWaves + w];
+    pre += w < wid ? c : 0;
+    tot += c;
+  }
+  const int r = base + pre + below(m, lane);
+  base += tot;
+  return r;
 }
 
 __device__ __forceinline__ int block_sum_int(int x, BigShared &B) {
@@ -2007,16 +2061,16 @@ __device__ __forceinline__ int block_min_int(int x, BigShared &B) {
 // FirstFit / BestFit act fused with the action phase (heuristic_apply, block form).
 template <int SPT>
 __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &L, const Tables &T,
-                                                 BigShared &B, uint32_t (&wa)[SPT], int policy,
-                                                 int32_t *act_out, uint8_t *valid_out) {
+                                                 BigShared &B, uint32_t LDSP *W, int policy,
+                                                 int32_t *act_out, uint8_t *valid_out STAMP_PARAMS) {
   const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P, NW = p.NW;
   const bool bf = policy == 1;
   uint32_t pend = 0;
-#pragma unroll 1
+VMP_SLOOP
   for (int s = 0; s < SPT; s++)
-    if (w_pl(wa[s]) == WAIT) pend |= 1u << s;
+    if (w_pl(W[s * NT + t]) == WAIT) pend |= 1u << s;
   uint32_t won = 0, bad = 0;
   int64_t n_place = 0;
   if (block_sum_int(pend != 0, B) > 0) {
@@ -2039,32 +2093,30 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
         if (w0) build_bitmaps(p, L, false);
         __syncthreads();
         hit = 0;
-#pragma unroll 1
+VMP_SLOOP
         for (int s = 0; s < SPT; s++)
-          if (((pend >> s) & 1u) && bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) >= 0)
-            hit |= 1u << s;
+          if ((pend >> s) & 1u) {
+            const uint32_t w = W[s * NT + t];
+            if (bm_query(L, NW, w_cc(w), w_cm(w)) >= 0) hit |= 1u << s;
+          }
         rebuild = false;
+        STAMP(17);
       }
       // earliest VM (index order) with a fit
       int mine = 0x7fffffff;
-#pragma unroll 1
+VMP_SLOOP
       for (int s = SPT - 1; s >= 0; s--)
         if ((hit >> s) & 1u) mine = s * NT + t;
       const int vw = block_min_int(mine, B);
       if (vw == 0x7fffffff) break;
-#pragma unroll 1
+VMP_SLOOP
       for (int s = 0; s < SPT; s++)
         if (s * NT + t <= vw) pend &= ~(1u << s);
       hit &= pend;
       const int ws = vw / NT, wt = vw - ws * NT;
-      if (t == wt) {
-#pragma unroll 1
-        for (int s = 0; s < SPT; s++)
-          if (s == ws) B.bc[0] = (int32_t)wa[s];
-      }
-      __syncthreads();
-      const uint32_t ww = (uint32_t)B.bc[0];
+      const uint32_t ww = W[vw];
       const int kc = w_cc(ww), km = w_cm(ww);
+      STAMP(18);
       if (w0) {
         const int q = bf ? bf_choose(p, L, kc, km) : bm_query(L, NW, kc, km);
         const bool ok = env_place(L, T, q, kc, km);
@@ -2105,37 +2157,36 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
         }
       }
       __syncthreads();
+      STAMP(19);
       const int q = B.bc[1];
       const bool ok = B.bc[2] != 0;
       n_place += ok;
       if (t == wt) {
-#pragma unroll 1
-        for (int s = 0; s < SPT; s++)
-          if (s == ws) {
-            won |= 1u << s;
-            if (ok) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)q;
-            else bad |= 1u << s;
-          }
+        won |= 1u << ws;
+        if (ok) W[vw] = (ww & 0xFFFF0000u) | (uint32_t)q;
+        else bad |= 1u << ws;
         if (act_out) act_out[vw] = q;
       }
       {  // re-query the VMs q fitted before and not after
         const int tq = B.bc[4], tc_old = B.bc[3], tmq = B.bc[5], tm_old = B.bc[7];
-#pragma unroll 1
+VMP_SLOOP
         for (int s = 0; s < SPT; s++) {
-          const int c = w_cc(wa[s]), m = w_cm(wa[s]);
-          if (((hit >> s) & 1u) && c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) &&
-              bm_query(L, NW, c, m) < 0)
+          if (!((hit >> s) & 1u)) continue;
+          const uint32_t w = W[s * NT + t];
+          const int c = w_cc(w), m = w_cm(w);
+          if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && bm_query(L, NW, c, m) < 0)
             hit &= ~(1u << s);
         }
       }
     }
   }
   if (act_out || valid_out) {
-#pragma unroll 1
+VMP_SLOOP
     for (int s = 0; s < SPT; s++) {
       const int v = s * NT + t;
-      if (live(wa[s])) {
-        if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(wa[s]);
+      const uint32_t w = W[v];
+      if (live(w)) {
+        if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(w);
         if (valid_out) valid_out[v] = (uint8_t)!((bad >> s) & 1u);
       }
     }
@@ -2148,23 +2199,24 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
 // are compacted in ascending VM order and applied by wave 0 one by one.
 template <int SPT>
 __device__ __forceinline__ void big_external(const EnvParams &p, const Lds &L, const Tables &T,
-                                             BigShared &B, uint32_t (&wa)[SPT],
+                                             BigShared &B, uint32_t LDSP *W,
                                              const int32_t *act_row, uint8_t *valid_out,
                                              int64_t &n_place, int64_t &n_susp) {
   const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
   const int P = p.P, WAIT = p.P;
-#pragma unroll 1
+VMP_SLOOP
   for (int s = 0; s < SPT; s++) {
     const int v = s * NT + t;
-    const bool in = live(wa[s]);
-    const int c = w_pl(wa[s]);
+    const uint32_t wv = W[v];
+    const bool in = live(wv);
+    const int c = w_pl(wv);
     const int tg = in ? act_row[v] : c;
     const bool isplace = in && c == WAIT && tg >= 0 && tg < P;
     const bool issusp = in && c < P && tg == WAIT;
     int nev = 0;
     const int r = bcx_rank(isplace || issusp, B, nev);
     if (isplace || issusp) {
-      B.evw[r] = wa[s];
+      B.evw[r] = wv;
       B.evt[r] = tg;
     }
     __syncthreads();
@@ -2202,7 +2254,7 @@ __device__ __forceinline__ void big_external(const EnvParams &p, const Lds &L, c
     if (isplace) ok = B.evok[r] != 0;
     n_place += block_sum_int(isplace && ok, B);
     n_susp += block_sum_int(issusp, B);
-    if (ok && tg != c && in) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)tg;
+    if (ok && tg != c && in) W[v] = (wv & 0xFFFF0000u) | (uint32_t)tg;
     if (valid_out && in) valid_out[v] = (uint8_t)ok;
   }
 }
@@ -2321,24 +2373,33 @@ __device__ __noinline__ void big_predraw(const EnvParams &p, const Tables &T, ch
 // _run_vms, _accept_vm_requests, stats + reward, termination (env_tail, block form).
 template <int SPT>
 __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, const Tables &T,
-                                           BigShared &B, uint32_t (&wa)[SPT],
-                                           uint32_t (&rem)[SPT], int kstep, bool &terminated) {
-  const int t = threadIdx.x, lane = lane_id();
+                                           BigShared &B, uint32_t LDSP *W,
+                                           uint32_t (&rem)[SPT], int kstep,
+                                           bool &terminated STAMP_PARAMS) {
+  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
   EnvHdr LDSP *H = L.hdr;
-  // ---- _run_vms ----
-  int64_t n_term = 0;
-#pragma unroll 1
-  for (int s = 0; s < SPT; s++) {
-    const bool running = w_pl(wa[s]) < P;
+  // ---- _run_vms: decrement, then free the finishers in ascending VM order ----
+  uint32_t fterm = 0;
+#pragma unroll
+  for (int s = 0; s < SPT; s++) {  // rem[] statically indexed: stays in registers
+    const bool running = w_pl(W[s * NT + t]) < P;
     if (running && rem[s] > 0) rem[s] -= 1;
-    const bool term = running && rem[s] == 0;
-    int nt = 0;
-    const int r = bcx_rank(term, B, nt);
-    if (term) B.evw[r] = wa[s];
+    if (running && rem[s] == 0) fterm |= 1u << s;
+  }
+  const int n_term = row_counts<SPT>(fterm, B);
+#pragma unroll 1
+  for (int j0 = 0; j0 < n_term; j0 += 512) {
+    int base = 0;
+VMP_SLOOP
+    for (int s = 0; s < SPT; s++) {
+      const int r = slot_rank(fterm, s, B, base);
+      if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) B.evw[r - j0] = W[s * NT + t];
+    }
     __syncthreads();
     if (w0) {
+      const int nt = n_term - j0 < 512 ? n_term - j0 : 512;
 #pragma unroll 1
       for (int i = 0; i < nt; i++) {  // frees in ascending VM order
         const uint32_t ew = B.evw[i];
@@ -2353,32 +2414,25 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
         wsync();
       }
     }
-    n_term += nt;
-    if (term) {
-      wa[s] = w_make(NUL, 0, 0);
-      rem[s] = 0;
-    }
+    __syncthreads();
   }
-  __syncthreads();
+VMP_SLOOP
+  for (int s = 0; s < SPT; s++)
+    if ((fterm >> s) & 1u) W[s * NT + t] = w_make(NUL, 0, 0);
+  STAMP(2);
   if (w0)
     for (int i = lane; i < P; i += 64) {  // precision clamp
       if (L.cpu[i] < 1e-7) L.cpu[i] = 0;
       if (L.mem[i] < 1e-7) L.mem[i] = 0;
     }
   // ---- _accept_vm_requests: the first k NULL slots in VM order ----
-  int n_null = 0;
-  int nrank[SPT];
-#pragma unroll 1
-  for (int s = 0; s < SPT; s++) {
-    const bool isnull = w_pl(wa[s]) == NUL;
-    int nn = 0;
-    const int r = bcx_rank(isnull, B, nn);
-    nrank[s] = isnull ? n_null + r : 0x7fffffff;
-    n_null += nn;
-  }
+  uint32_t fnull = 0;
+VMP_SLOOP
+  for (int s = 0; s < SPT; s++)
+    if (w_pl(W[s * NT + t]) == NUL) fnull |= 1u << s;
+  const int n_null = row_counts<SPT>(fnull, B);
   const int64_t arrivals = L.arr[kstep];
   const int64_t k = arrivals < n_null ? arrivals : n_null;
-  __syncthreads();
   if (k > 0) {
     Pcg r1 = ld_pcg(H, 0), r2 = ld_pcg(H, 1);
 #pragma unroll 1
@@ -2398,11 +2452,12 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
         }
       }
       __syncthreads();
-#pragma unroll 1
-      for (int s = 0; s < SPT; s++) {
-        const int j = nrank[s];
-        if (j >= j0 && j < j1) {
-          wa[s] = w_make(WAIT, L.accc[j], L.accm[j]);
+      int base = 0;
+#pragma unroll
+      for (int s = 0; s < SPT; s++) {  // rem[] statically indexed
+        const int j = slot_rank(fnull, s, B, base);
+        if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
+          W[s * NT + t] = w_make(WAIT, L.accc[j], L.accm[j]);
           rem[s] = (uint32_t)B.evt[j - j0];
         }
       }
@@ -2414,26 +2469,36 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
     }
   }
   __syncthreads();
+  STAMP(3);
   // ---- stats + reward ----
   const bool kl = p.reward == 2;
-  int n_ex = 0, n_w = 0;
-#pragma unroll 1
+  uint32_t fex = 0;
+  int n_w = 0;
+VMP_SLOOP
   for (int s = 0; s < SPT; s++) {
-    const int c = w_pl(wa[s]);
-    const bool ex = c <= WAIT;
-    int ne = 0;
-    const int r = bcx_rank(ex, B, ne);
-    if (kl && ex) {
-      L.ccomp[n_ex + r] = (uint8_t)w_cc(wa[s]);
-      L.mcomp[n_ex + r] = (uint8_t)w_cm(wa[s]);
-    }
-    n_ex += ne;
+    const int c = w_pl(W[s * NT + t]);
+    if (c <= WAIT) fex |= 1u << s;
     n_w += c == WAIT;
   }
   n_w = block_sum_int(n_w, B);
+  const int n_ex = row_counts<SPT>(fex, B);
+  if (kl) {
+    int base = 0;
+VMP_SLOOP
+    for (int s = 0; s < SPT; s++) {
+      const int r = slot_rank(fex, s, B, base);
+      if ((fex >> s) & 1u) {
+        const uint32_t w = W[s * NT + t];
+        L.ccomp[r] = (uint8_t)w_cc(w);
+        L.mcomp[r] = (uint8_t)w_cm(w);
+      }
+    }
+  }
   __syncthreads();
+  STAMP(11);
   if (w0) big_stats(p, T, B, L.base, k, n_ex, n_w, n_term, arrivals);
   __syncthreads();
+  STAMP(12);
   const double reward = __longlong_as_double(B.b64[0]);
   terminated = B.bc[6] != 0;
   __syncthreads();
@@ -2449,7 +2514,9 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   const bool w0 = t < 64;
   const int e = blockIdx.x;
   const Lds L = make_lds(p, (char LDSP *)lds);
+  uint32_t LDSP *W = reinterpret_cast<uint32_t LDSP *>((char LDSP *)lds + p.lds_wave_bytes);
   const int V = p.V, P = p.P;
+  STAMP_DECL
   for (int i = t; i < 128; i += NT) {
     T.cent[i] = (double)i / 100.0;
     T.fcent[i] = (float)((double)i / 100.0);
@@ -2459,21 +2526,24 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   if (t < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[t] = reinterpret_cast<const uint64_t *>(p.hdr + e)[t];
   const double *pm = p.pm + (int64_t)e * 2 * P;
   for (int i = t; i < 2 * P; i += NT) L.cpu[i] = pm[i];
+  for (int i = t; i < kBigMaxSPT * kBigMaxWaves; i += NT) B.rc[i] = 0;
   const uint64_t *vmw = p.vmw + (int64_t)e * V;
-  uint32_t wa[SPT], rem[SPT];
-#pragma unroll 1
-  for (int s = 0; s < SPT; s++) {
+  uint32_t rem[SPT];
+#pragma unroll
+  for (int s = 0; s < SPT; s++) {  // all loads in flight at once; rem[] in registers
     const int v = s * NT + t;
     const uint64_t w = v < V ? vmw[v] : (uint64_t)kPad;
-    wa[s] = (uint32_t)w;
+    W[v] = (uint32_t)w;
     rem[s] = (uint32_t)(w >> 32);
   }
   __syncthreads();
+  STAMP(13);
   if (o.k_steps > 0 && w0) {
     const uint64_t *jt = p.jump + 4 * lane;
     big_predraw(p, T, L.base, o.k_steps, jt);
   }
   __syncthreads();
+  STAMP(14);
   bool term = false;
   int64_t ndone = 0;
 #pragma unroll 1
@@ -2483,16 +2553,17 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
     int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
     int64_t n_place = 0, n_susp = 0;
     if (o.policy >= 0)
-      n_place = big_heuristic<SPT>(p, L, T, B, wa, o.policy, act_row, valid_row);
+      n_place = big_heuristic<SPT>(p, L, T, B, W, o.policy, act_row, valid_row STAMP_ARGS);
     else
-      big_external<SPT>(p, L, T, B, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
+      big_external<SPT>(p, L, T, B, W, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
     __syncthreads();
+    STAMP(16);
     if (t == 0) {
       L.hdr->place_action += n_place;
       L.hdr->suspend_action += n_susp;
     }
     __syncthreads();
-    const double r = big_tail<SPT>(p, L, T, B, wa, rem, k, term);
+    const double r = big_tail<SPT>(p, L, T, B, W, rem, k, term STAMP_ARGS);
     if (o.reward && t == 0) o.reward[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
@@ -2500,21 +2571,22 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
     if (w0) svc_commit(L);
   }
   if (o.k_steps == 0 && o.policy >= 0 && o.act_out) {
-    uint32_t wt[SPT];
-#pragma unroll 1
-    for (int s = 0; s < SPT; s++) wt[s] = wa[s];
-    big_heuristic<SPT>(p, L, T, B, wt, o.policy, o.act_out + (int64_t)e * V, nullptr);
+    big_heuristic<SPT>(p, L, T, B, W, o.policy, o.act_out + (int64_t)e * V, nullptr STAMP_ARGS);
+    __syncthreads();
+    for (int v = t; v < V; v += NT) W[v] = (uint32_t)vmw[v];  // act only: placements unchanged
   }
   __syncthreads();
+  STAMP(4);
   if (o.obs) {
     float *obs = o.obs + (int64_t)e * p.D;
-#pragma unroll 1
+VMP_SLOOP
     for (int s = 0; s < SPT; s++) {
       const int v = s * NT + t;
-      if (live(wa[s])) {
-        ST_NT(obs + v, (float)w_pl(wa[s]));
-        ST_NT(obs + V + v, T.fcent[w_cc(wa[s])]);
-        ST_NT(obs + 2 * V + v, T.fcent[w_cm(wa[s])]);
+      const uint32_t w = W[v];
+      if (live(w)) {
+        ST_NT(obs + v, (float)w_pl(w));
+        ST_NT(obs + V + v, T.fcent[w_cc(w)]);
+        ST_NT(obs + 2 * V + v, T.fcent[w_cm(w)]);
       }
     }
     for (int i = t; i < P; i += NT) {
@@ -2524,16 +2596,17 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   }
   if (o.mask_bits) {
     uint32_t *bits = o.mask_bits + (int64_t)e * V * p.W32;
-    const int A = p.A, W = p.W32, WAIT = p.P, NUL = p.P + 1;
-#pragma unroll 1
+    const int A = p.A, NW32 = p.W32, WAIT = p.P, NUL = p.P + 1;
+VMP_SLOOP
     for (int s = 0; s < SPT; s++) {
       const int v = s * NT + t;
-      const bool in = live(wa[s]);
-      const int c = in ? w_pl(wa[s]) : NUL;
-      const double vc = T.cent[w_cc(wa[s])], vm = T.cent[w_cm(wa[s])];
+      const uint32_t wv = W[v];
+      const bool in = live(wv);
+      const int c = in ? w_pl(wv) : NUL;
+      const double vc = T.cent[w_cc(wv)], vm = T.cent[w_cm(wv)];
       const bool waiting = in && c == WAIT;
 #pragma unroll 1
-      for (int w = 0; w < W; w++) {
+      for (int w = 0; w < NW32; w++) {
         uint32_t word = 0xFFFFFFFFu;
         const int a0 = w * 32;
         if (c >= a0 && c < a0 + 32 && c < A) word &= ~(1u << (c - a0));
@@ -2546,7 +2619,7 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
             if (fit) word &= ~(1u << (q - a0));
           }
         }
-        if (in) bits[(int64_t)v * W + w] = word;
+        if (in) bits[(int64_t)v * NW32 + w] = word;
       }
     }
   }
@@ -2554,16 +2627,22 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
     if (o.done && t == 0) o.done[e] = (uint8_t)term;
     if (o.done_count && t == 0) o.done_count[e] += ndone;
     uint64_t *vmo = p.vmw + (int64_t)e * V;
-#pragma unroll 1
+#pragma unroll
     for (int s = 0; s < SPT; s++) {
       const int v = s * NT + t;
-      if (live(wa[s])) ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rem[s] << 32));
+      const uint32_t w = W[v];
+      if (live(w)) ST_NT(vmo + v, (uint64_t)w | ((uint64_t)rem[s] << 32));
     }
     double *pmo = p.pm + (int64_t)e * 2 * P;
     for (int i = t; i < 2 * P; i += NT) ST_NT(pmo + i, (double)L.cpu[i]);
     if (t < 32)
       reinterpret_cast<uint64_t *>(p.hdr + e)[t] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
   }
+#ifdef VMP_STAMPS
+  STAMP(6);
+  if (p.stamps && t == 0)
+    for (int _i = 0; _i < kStamps; _i++) p.stamps[(int64_t)e * kStamps + _i] += st_acc[_i];
+#endif
 }
 template __global__ void k_env_big<4>(EnvParams, StepOut);
 template __global__ void k_env_big<8>(EnvParams, StepOut);
