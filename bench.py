@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--no-ppo", action="store_true", help="skip the PPO train / eval legs")
     ap.add_argument("--ppo-envs", type=int, default=8192, help="PPO training envs per GPU")
     ap.add_argument("--ppo-eval-envs", type=int, default=4096)
+    ap.add_argument("--ext-steps", type=int, default=50, help="external-action leg steps")
+    ap.add_argument("--stress-ff", type=int, default=2000, help="C5 fast-forward (2*L)")
+    ap.add_argument("--stress-steps", type=int, default=20)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -85,7 +88,8 @@ def main():
     N = args.envs
     P, V = CFG["pms"], CFG["vms"]
     D = 3 * V + 2 * P
-    seeds = 4 * (rank * N + np.arange(N, dtype=np.int64))
+    from vmp.replicas import shard_seeds
+    seeds = shard_seeds(rank, N)  # 4 * global env index
     env = BatchedVmEnv(Config(**CFG), N, seeds=seeds, device=dev)
     env.eval(False)
     L = _lib.lib()
@@ -137,6 +141,10 @@ def main():
         elapsed, kern_ms = float(t[0]), float(t[1])
     value = world * N * K / elapsed
 
+    # ---- external-action mode (the PPO path): vmp_step on i32[N, V] actions ----
+    ext = _guard(bench_external, args, env, dev, stream, dist, world, P, V)
+    ext_steps = args.ext_steps + 2 if isinstance(ext, dict) and "error" not in ext else 0
+
     # ---- fused K-step rollout (state resident on chip), same envs ----
     kr = args.rollout_k
     rbuf = torch.empty((kr, N), dtype=torch.float64, device=dev)
@@ -157,7 +165,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         r_el = float(t[0])
     fused_value = world * N * kr * nrep / r_el
-    steps_done = args.ff_steps + args.warmup + K + kr * (nrep + 1)
+    steps_done = args.ff_steps + args.warmup + K + ext_steps + kr * (nrep + 1)
+
+    # ---- replica reduction: counters summed, per-env returns of the
+    # last fused rollout gathered over ranks (RCCL at N > 1) ----
+    from vmp.replicas import reduce_replicas
+    ctr_sum, ret_all = reduce_replicas(env.counters(), rbuf.sum(0), dist)
+    replicas = {"counters_sum": [int(x) for x in ctr_sum.cpu().tolist()],
+                "counters": ["total_requests", "served", "suspend_action", "place_action",
+                             "dropped", "timestep"],
+                "returns_gathered": int(ret_all.numel()),
+                "return_mean": float(ret_all.mean()),
+                "return_steps": kr,
+                "collectives": ("all_reduce(int64 counters, SUM) + all_gather(f64 returns) "
+                                f"over {'RCCL' if world > 1 else 'none (1 rank)'}")}
 
     # ---- reward MAE / counter equality vs the CPU oracle on sampled envs ----
     parity = None
@@ -223,7 +244,10 @@ def main():
                      "kernel": "vmp::k_env<16, true> (heuristic act+step, one step per launch)", "kernel_ms": kern_ms,
                      "bytes_per_env_step": bpe},
         "cpu_baseline": cpu,
+        "reference_cpu": _reference_cpu(),
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},
+        "external_actions": ext,
+        "replicas": replicas,
         "parity": parity,
         "ppo_train": ppo_train,
         "ppo_train_bf16": ppo_train_bf16,
@@ -300,7 +324,10 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
 def bench_stress(args, dev, rank, world, dist):
     """BASELINE config 5: P1000 / V10000 at 100 % load
     (lambda = 1000/0.55/1000), L = 1000, reward kl, BestFit act + step, 512 envs
-    per GPU on the block-per-env kernel; 100 fast-forward steps, then 10 timed."""
+    per GPU on the block-per-env kernel k_env_big. Fast-forwarded 2*L = 2000
+    steps with the fused rollout (steady state: ~1600 running / ~380 waiting VMs
+    per env), then K timed per-step launches; kernel time from HIP events on
+    the launch stream."""
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
     from vmp import _lib
@@ -309,30 +336,114 @@ def bench_stress(args, dev, rank, world, dist):
                  training_steps=10000, eval_steps=100000, seed=0, reward_function="kl",
                  sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
     env = BatchedVmEnv(cfg, N, seeds=4 * (rank * N + np.arange(N, dtype=np.int64)), device=dev)
-    env.rollout("bestfit", 100)
+    left = args.stress_ff
+    while left > 0:
+        env.rollout("bestfit", min(250, left))
+        left -= 250
     obs = torch.empty((N, env.D), dtype=torch.float32, device=dev)
     rew = torch.empty((N,), dtype=torch.float64, device=dev)
     done = torch.empty((N,), dtype=torch.uint8, device=dev)
     L, h = _lib.lib(), env._bind()
+    stream = torch.cuda.current_stream(dev)
+    pl = env.state()["vm_placement"]
+    running, waiting = float((pl < P).sum(1).double().mean()), float((pl == P).sum(1).double().mean())
+    del pl
+    _lib.check(L.vmp_heuristic_step(h, 1, None, _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done), None))
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
-    K = 10
+    K = args.stress_steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
     t0 = time.perf_counter()
-    for _ in range(K):
+    for a, b in ev:
+        a.record(stream)
         _lib.check(L.vmp_heuristic_step(h, 1, None, _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done),
                                         None))
+        b.record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    kern_ms = _max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in ev])), dev, dist)
     env.close()
     bpe = step_bytes(P, V)
+    ach = bpe * N / (kern_ms * 1e-3) / 1e9
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
             "workload": "P1000 V10000, lambda 1.818, L 1000, reward kl, BestFit act + step "
                         "(k_env_big, one workgroup per env)", "envs_per_gpu": N,
-            "ms_per_step": 1e3 * el / K, "bytes_per_env_step": bpe,
-            "hbm_frac": bpe * N * K / el / (HBM_PEAK_GBS * 1e9)}
+            "ff_steps": args.stress_ff, "steps": K, "mean_running": running,
+            "mean_waiting": waiting, "ms_per_step": 1e3 * el / K, "kernel_ms": kern_ms,
+            "bytes_per_env_step": bpe,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "kernel": "vmp::k_env_big<20>"}}
+
+
+def bench_external(args, env, dev, stream, dist, world, P, V):
+    """SURVEY §8(d) C-main, external-action mode (the path PPO drives): per step
+    the FirstFit action of every env is produced by an act-only launch
+    (vmp_heuristic_act, untimed by the events) into an i32[N, V] buffer, then
+    vmp_step (VmEnv.step, env.py:66-103) consumes it, writing obs / reward /
+    done. Kernel time = HIP events around vmp_step only; the wall rate counts
+    both launches."""
+    from vmp import _lib
+    N = env.n_envs
+    L, h = _lib.lib(), env._bind()
+    D = 3 * V + 2 * P
+    act = torch.empty((N, V), dtype=torch.int32, device=dev)
+    obs = torch.empty((N, D), dtype=torch.float32, device=dev)
+    rew = torch.empty((N,), dtype=torch.float64, device=dev)
+    done = torch.empty((N,), dtype=torch.uint8, device=dev)
+    pa, po, pr, pd = _lib.ptr(act), _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done)
+
+    def one(e0=None, e1=None):
+        _lib.check(L.vmp_heuristic_act(h, 0, pa))
+        if e0 is not None:
+            e0.record(stream)
+        _lib.check(L.vmp_step(h, pa, po, pr, pd, None))
+        if e1 is not None:
+            e1.record(stream)
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    K = args.ext_steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        one(a, b)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    kern_ms = _max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in ev])), dev, dist)
+    bpe = step_bytes(P, V) + 4 * V
+    ach = bpe * N / (kern_ms * 1e-3) / 1e9
+    return {"value": world * N / (kern_ms * 1e-3), "unit": "env-steps/s",
+            "value_kind": "step kernel alone (events around vmp_step)",
+            "act_plus_step_wall": world * N * K / el, "steps": K, "kernel_ms": kern_ms,
+            "bytes_per_env_step": bpe,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS,
+                         "kernel": "vmp::k_env<16, true> (external actions)"}}
+
+
+def _reference_cpu():
+    """The unmodified reference VmEnv.step timed in the build container
+    (tools/time_reference.py -> tests/golden/ref_cpu_timing.json): a different
+    box from this run's; carried for context beside cpu_baseline."""
+    pth = os.path.join(ROOT, "tests", "golden", "ref_cpu_timing.json")
+    if not os.path.exists(pth):
+        return None
+    d = json.load(open(pth))
+    r = d["results"].get("p100v1000", {})
+    return {"value": r.get("single_core_steps_per_s"), "unit": "env-steps/s", "cores": 1,
+            "kind": "reference (unmodified Python VmEnv.step)",
+            "procs_8_aggregate": r.get("procs_8_aggregate_steps_per_s"),
+            "box": "build container, not the GPU box: " + str(d["box"].get("model")),
+            "sample": d["what"]}
 
 
 def bench_ppo_eval(args, dev, rank, world, dist):

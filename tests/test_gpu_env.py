@@ -88,10 +88,14 @@ def test_trajectory_replay_hip(name, big, monkeypatch):
             assert int(b0.rank()[0]) == d["rank"][t]
 
 
+@pytest.mark.parametrize("big", [False, True], ids=["wave", "block"])
 @pytest.mark.parametrize("name", [n for n in T.traj_names() if n.endswith("pure")] +
                          ["c1_10yml_ff"])
-def test_heuristic_act_hip(name):
+def test_heuristic_act_hip(name, big, monkeypatch):
+    """Act-only launches (vmp_heuristic_act, k_steps == 0) of both env kernels."""
     from vmp.batched import BatchedVmEnv
+    if big:
+        monkeypatch.setenv("VMP_BIG_KERNEL", "1")
     d = T.load(name)
     b = BatchedVmEnv(_cfg(d["config"]), 1, seeds=[d["config"]["seed"]], device=DEV)
     b.eval(True)
@@ -268,8 +272,10 @@ def test_large_v_block_kernel_vs_oracle(policy, reward):
                 _, rew, _, _ = b.step(torch.tensor(a, dtype=torch.int32, device=DEV))
                 acts = a
             else:
+                pre = b.heuristic_act(policy).cpu().numpy()  # act-only launch
                 _, rew, _, _, act = b.heuristic_step(policy, want_actions=True)
                 acts = act.cpu().numpy()
+                assert np.array_equal(pre, acts), (P, V, t)
             rew = rew.cpu().numpy()
             for i, e in enumerate(orc):
                 if policy is not None:
@@ -284,3 +290,52 @@ def test_large_v_block_kernel_vs_oracle(policy, reward):
             assert np.array_equal(sd["cpu"][i].cpu().numpy(), so[3]), (P, V)
             assert np.array_equal(b.counters()[i].cpu().numpy(), e.counters()[0]), (P, V)
         b.close()
+
+
+def test_c5_steady_state_bestfit_kl_vs_oracle():
+    """BASELINE config 5 (P1000 / V10000, lambda = 1000/0.55/1000,
+    L = 1000, reward kl, BestFit) from reset through the 2·L-step fill into the
+    steady state (~1600 running and ~380 waiting VMs per env): 2000 fused
+    rollout steps whose every reward must equal the oracle's, then 200 per-step
+    act+step launches checked on actions, rewards and observations, then the
+    full state and counters. Seeds 4·i as bench.py's."""
+    from vmp.batched import BatchedVmEnv
+    P, V = 1000, 10000
+    cfg = dict(pms=P, vms=V, arrival_rate=round(1000 / 0.55 / 1000, 3), service_length=1000,
+               training_steps=10000, eval_steps=100000, seed=0, reward_function="kl",
+               sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
+    seeds = np.array([0, 4], dtype=np.int64)
+    b = BatchedVmEnv(_cfg(cfg), 2, seeds=seeds, device=DEV)
+    b.eval(True)
+    orc = [O.OracleEnv(dict(cfg, seed=int(s))) for s in seeds]
+    for e, s in zip(orc, seeds):
+        e.eval(True)
+        e.reset(int(s))
+    FF, T_CHECK = 2000, 200
+    for k0 in range(0, FF, 250):
+        rs, _ = b.rollout("bestfit", 250)
+        rs = rs.cpu().numpy()
+        for k in range(250):
+            for i, e in enumerate(orc):
+                _, r, _, _ = e.step(e.bestfit())
+                assert T.kl_close(rs[k, i], r), (k0 + k, i, rs[k, i], r)
+    pl = b.state()["vm_placement"].cpu().numpy()
+    assert (pl < P).sum(1).min() > 1400 and (pl == P).sum(1).min() > 100, "not at steady state"
+    for t in range(T_CHECK):
+        obs, rew, _, _, act = b.heuristic_step("bestfit", want_actions=True)
+        rew, act, obs = rew.cpu().numpy(), act.cpu().numpy(), obs.cpu().numpy()
+        for i, e in enumerate(orc):
+            a = e.bestfit()
+            assert np.array_equal(a, act[i]), (t, i)
+            o, r, _, _ = e.step(a)
+            assert T.kl_close(rew[i], r), (t, i, rew[i], r)
+            assert np.array_equal(o, obs[i]), (t, i)
+    sd = b.state()
+    ctr = b.counters().cpu().numpy()
+    for i, e in enumerate(orc):
+        so = e.state()
+        for j, k in enumerate(("vm_placement", "vm_cpu", "vm_memory", "cpu", "memory",
+                               "vm_remaining_runtime")):
+            assert np.array_equal(sd[k][i].cpu().numpy(), so[j]), (k, i)
+        assert np.array_equal(ctr[i], e.counters()[0]), i
+    b.close()

@@ -1,9 +1,9 @@
 """Device Record metrics (vmp_record_*, record.py:34-134) on the MI355X:
 every published firstfit/bestfit row of data/exp_suspension/data.csv (100k-step
 evals of config/100.yml: served, valid suspends, valid actions, mean life,
-mean pending, mean/max slowdown) and the literal Record restatement
-(vmp/record.py, fed by Base.record_testing_step from eval-mode info) on a
-trajectory with random suspensions and placements."""
+mean pending, mean/max slowdown) and the literal host restatement of
+record.py (tests/record_literal.py, fed by Base.record_testing_step from
+eval-mode info) on a trajectory with random suspensions and placements."""
 import csv
 import os
 
@@ -97,7 +97,8 @@ def test_device_record_matches_literal_record(seed):
         a = _random_actions(env._b, g)
         obs, reward, done, _, info = env.step(a)
         base.record_testing_step(reward, info)
-    lit = base.record.get_summary()
+    from tests import record_literal
+    lit = record_literal.summary(vars(base.record), cfg.pms)
     dev = env._b.record_summary()[0]
     assert lit["total suspend actions"] > 0
     for k, v in lit.items():
@@ -108,4 +109,27 @@ def test_device_record_matches_literal_record(seed):
     for k in ("average VM life", "average pending", "median pending", "max pending",
               "average slowdown", "median slowdown", "max slowdown", "drop rate", "rank mean"):
         assert dev[k] == lit[k], (k, dev[k], lit[k])
+    env.close()
+
+
+def test_base_test_summary_is_the_device_summary(tmp_path):
+    """Base.test (base.py:63-118) returns a Record whose summary comes from the
+    device recorder; it equals the host restatement on the recorded traces,
+    and a saved record re-imports with that summary (record.py:136-168)."""
+    import json
+    from tests import record_literal
+    from vmp.agents import FirstFitAgent
+    from vmp.config import Config
+    from vmp.env import VmEnv
+    from vmp.record import Record
+    cfg = Config(pms=10, vms=30, arrival_rate=0.9, service_length=40, training_steps=1000,
+                 eval_steps=400, seed=7, reward_function="ut", allow_null_action=True)
+    env = VmEnv(cfg, device="cuda:0")
+    rec = FirstFitAgent(env).test(output=str(tmp_path / "r.json"))
+    got, lit = rec.get_summary(), record_literal.summary(vars(rec), cfg.pms)
+    assert list(got) == list(lit)
+    for k, v in lit.items():
+        assert abs(float(got[k]) - float(v)) <= 1e-3 + 1e-9 * abs(float(v)), (k, got[k], v)
+    back = Record.import_record("FirstFitAgent", json.load(open(tmp_path / "r.json")))
+    assert back.get_summary() == json.loads(json.dumps(got, default=float))
     env.close()

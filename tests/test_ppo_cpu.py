@@ -193,6 +193,42 @@ def test_data_parallel_update_equals_single_process():
         assert np.array_equal(res[0][0][k], res[1][0][k])
 
 
+def _rank_rng_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from vmp.ppo import PPOTrainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)  # every rank alike, as bench.py / vmp.main do
+        ag = _agent(n_envs=2)
+        PPOTrainer(ag, allocate=False)
+        logits = torch.zeros((4, 30 * 12))  # uniform Categoricals: only the stream decides
+        act, _, _ = ag.model.head(logits)
+        q.put((rank, ag.model.rng.seed, act.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_ranks_sample_independently():
+    """ranks seeded alike must not draw the same actions for equal
+    logits (their HeadRng streams are folded with the rank); rank 0 keeps the
+    single-process stream."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_rng_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (s, a)) for r, s, a in (q.get(timeout=240) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    assert res[0][0] == _agent(n_envs=2).model.rng.seed
+    assert res[0][0] != res[1][0]
+    assert not np.array_equal(res[0][1], res[1][1])
+
+
 def test_weights_io_compiled_prefix(tmp_path):
     """save_model writes the reference's torch.compile keys; load_model reads both."""
     w = _golden("ppo10_wr_weights.npz")

@@ -23,7 +23,8 @@ def torch_head(logits, V, A, bits=None, action=None, rng=None, wait_ratio=-1.0, 
     # Categorical(logits=...): logits - logsumexp (ppo.py:121), rounded in f32 as torch does
     logp = lg - torch.logsumexp(lg, dim=-1, keepdim=True)
     if action is None:
-        g = torch.Generator(device=logits.device).manual_seed(int(rng.take(B * V)[1]) if rng else 0)
+        seed, off = rng.take(B * V) if rng else (0, 0)
+        g = torch.Generator(device=logits.device).manual_seed((seed ^ off) & (2**63 - 1))
         action = torch.multinomial(logp.exp().reshape(B * V, A).detach(), 1, generator=g).reshape(B, V)
     a = action.reshape(B, V).long()
     lp = logp.gather(-1, a[..., None]).squeeze(-1).sum(-1)

@@ -199,7 +199,7 @@ void carve(vmp_handle *h) {
   p.off_leaf = (int32_t)off;
   if (deep) off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);  // lo, len, lane-0 stack
   p.off_leafval = (int32_t)off;
-  if (deep) off = align16(off + 8 * 8 * (int64_t)p.n_leaf + 8 * (2 * (int64_t)p.n_leaf + 64));
+  if (deep) off = align16(off + 8 * (2 * (int64_t)p.n_leaf + 64));  // leaf sums + value stack
   p.off_pre = (int32_t)off;   // per-launch random draws follow (launch_env)
   p.lds_wave_bytes = (int32_t)off;
 }
@@ -268,6 +268,8 @@ extern "C" {
 int vmp_abi_version(void) { return VMP_ABI_VERSION; }
 const char *vmp_last_error(void) { return g_err.c_str(); }
 
+static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, const int64_t *seeds);
+
 int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32_t device,
                vmp_handle **out) {
   if (!cfg || !out || n_env <= 0 || !seeds) return fail(VMP_EINVAL, "null argument or n_env <= 0");
@@ -301,16 +303,28 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   int rc = setup_pois(cfg->arrival_rate, h->arr, &h->lg_arr, t1);
   if (rc == VMP_OK) rc = setup_pois(cfg->service_length, h->svc, &h->lg_svc, t2);
   if (rc != VMP_OK) {
-    delete h;
-    return rc;
+    const std::string msg = g_err;
+    vmp_destroy(h);  // frees whatever the first setup_pois allocated
+    return fail(rc, msg);
   }
+  rc = create_rest(h, cfg, n_env, seeds);
+  if (rc != VMP_OK) {
+    const std::string msg = g_err;
+    vmp_destroy(h);
+    return fail(rc, msg);
+  }
+  *out = h;
+  return VMP_OK;
+}
+
+// vmp_create after the handle exists: every failure returns a code and the
+// caller destroys the handle (vmp_destroy tolerates what was not allocated).
+static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, const int64_t *seeds) {
   hipError_t e1 = hipMalloc(&h->vmw, sizeof(uint64_t) * (size_t)n_env * h->V);
   hipError_t e2 = hipMalloc(&h->pm, sizeof(double) * (size_t)n_env * 2 * h->P);
   hipError_t e3 = hipMalloc(&h->hdr, sizeof(EnvHdr) * (size_t)n_env);
-  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
-    vmp_destroy(h);
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
     return fail(VMP_EOOM, "device allocation failed");
-  }
   HIP_TRY(hipMemset(h->hdr, 0, sizeof(EnvHdr) * (size_t)n_env));
   EnvParams &p = h->prm;
   p.N = h->N;
@@ -360,31 +374,29 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
   int maxn = h->V > h->P ? h->V : h->P;
   int depth = 0;
   for (int n = 0; n <= maxn; n++) depth = pw_depth(n) > depth ? pw_depth(n) : depth;
-  if (depth > 12) {
-    vmp_destroy(h);
+  if (depth > 12)
     return fail(VMP_EINVAL, "config exceeds the pairwise-sum recursion depth of this build");
-  }
   {
     const int64_t per_env = p.lds_wave_bytes + 20 * kSpecDraws + 4 * kMaxStepsPerLaunch;
     int spt = 0, nt = 0;
     if (h->big) big_shape(h->V, spt, nt);
     const int64_t need = h->big ? per_env + kBigStaticLds + 4 * (int64_t)spt * nt
                                 : per_env * kEnvWavesPerBlock + 2048;
-    if (need > 160 * 1024) {
-      vmp_destroy(h);
+    if (need > 160 * 1024)
       return fail(VMP_EINVAL, "config too large for the LDS carve of this build");
-    }
   }
   refresh_params(h);
   int64_t *dseeds = nullptr;
   HIP_TRY(hipMalloc(&dseeds, sizeof(int64_t) * n_env));
-  HIP_TRY(hipMemcpy(dseeds, seeds, sizeof(int64_t) * n_env, hipMemcpyHostToDevice));
-  dim3 grid((n_env + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
-  hipLaunchKernelGGL(k_reset, grid, block, 0, h->stream, h->prm, dseeds, nullptr, nullptr);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(h->stream));
-  HIP_TRY(hipFree(dseeds));
-  *out = h;
+  hipError_t e = hipMemcpy(dseeds, seeds, sizeof(int64_t) * n_env, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    dim3 grid((n_env + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
+    hipLaunchKernelGGL(k_reset, grid, block, 0, h->stream, h->prm, dseeds, nullptr, nullptr);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+  }
+  (void)hipFree(dseeds);
+  if (e != hipSuccess) return fail(VMP_EDEVICE, std::string("vmp_create reset: ") + hipGetErrorString(e));
   return VMP_OK;
 }
 
@@ -468,8 +480,9 @@ int vmp_heuristic_act(vmp_handle *h, int32_t policy, int32_t *actions) {
   return launch_env(h, o);
 }
 
-int vmp_heuristic_step(vmp_handle *h, int32_t policy, int32_t *actions_out, float *obs,
-                       double *reward, uint8_t *done, uint8_t *valid) {
+static int heuristic_step_impl(vmp_handle *h, int32_t policy, int32_t *actions_out, float *obs,
+                               double *reward, uint8_t *done, uint8_t *valid,
+                               int64_t *done_count) {
   if (!h) return fail(VMP_EINVAL, "null handle");
   if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
     return fail(VMP_EINVAL, "unknown policy");
@@ -479,6 +492,7 @@ int vmp_heuristic_step(vmp_handle *h, int32_t policy, int32_t *actions_out, floa
   o.obs = obs;
   o.reward = reward;
   o.done = done;
+  o.done_count = done_count;
   o.valid = valid;
   o.k_steps = 1;
   if (h->rec_on) {
@@ -491,6 +505,11 @@ int vmp_heuristic_step(vmp_handle *h, int32_t policy, int32_t *actions_out, floa
   return rc;
 }
 
+int vmp_heuristic_step(vmp_handle *h, int32_t policy, int32_t *actions_out, float *obs,
+                       double *reward, uint8_t *done, uint8_t *valid) {
+  return heuristic_step_impl(h, policy, actions_out, obs, reward, done, valid, nullptr);
+}
+
 int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double *rewards,
                           int64_t *done_count) {
   if (!h || k_steps < 1) return fail(VMP_EINVAL, "null handle or k_steps < 1");
@@ -498,12 +517,10 @@ int vmp_rollout_heuristic(vmp_handle *h, int32_t policy, int32_t k_steps, double
     return fail(VMP_EINVAL, "unknown policy");
   if (h->rec_on) {  // recorded: one step per launch, the recorder after each
     for (int32_t k = 0; k < k_steps; k++) {
-      int rc = vmp_heuristic_step(h, policy, nullptr, nullptr,
-                                  rewards ? rewards + (int64_t)k * h->N : nullptr, nullptr, nullptr);
+      int rc = heuristic_step_impl(h, policy, nullptr, nullptr,
+                                   rewards ? rewards + (int64_t)k * h->N : nullptr, nullptr,
+                                   nullptr, done_count);
       if (rc) return rc;
-      if (done_count) {
-        // done flags of recorded rollouts are not accumulated (eval loops stop at done)
-      }
     }
     return VMP_OK;
   }

@@ -249,7 +249,6 @@ constexpr int kStamps = 24;
 struct PwLds {
   int32_t LDSP *lo, *len;  // leaf list (DFS order), n_leaf entries
   int32_t LDSP *stk;            // lane-0 stack, 3 * 64 ints
-  double LDSP *acc;             // 8 accumulators per leaf
   double LDSP *val;             // leaf sums, + value stack
 };
 
@@ -316,9 +315,12 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   return __longlong_as_double((int64_t)(((uint64_t)hi << 32) | lo));
 }
 
-// Register-resident plan (depth <= kPwRegDepth, i.e. n <= 1928): leaf cnt's
-// (offset, size) lands in lane cnt; the combine reads leaf sums by readlane.
+// Register-resident plan (depth <= RD): leaf cnt's (offset, size) lands in
+// lane cnt; the combine reads leaf sums by readlane. pw_reg_cap(RD) is the
+// largest n such that every n' <= n splits into at most RD levels and 64
+// leaves (1928 for RD = 4, 7688 for RD = 6; host check: vmp_capi.cpp pw_depth).
 constexpr int kPwRegDepth = 4;
+constexpr int pw_reg_cap(int rd) { return rd <= 4 ? 1928 : rd == 5 ? 3848 : 7688; }
 template <int D>
 __device__ __forceinline__ void pw_enum_r(int o, int n, int &cnt, int lane, int &my_o,
                                           int &my_m) {
@@ -386,8 +388,9 @@ __device__ __forceinline__ double pw_leaf_group(int o, int m, F &f) {
   return res;
 }
 
-template <class F>
+template <int RD = kPwRegDepth, class F>
 __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
+  static_assert(RD >= 4 && RD <= 6, "register plan depth");
   const int lane = lane_id();
   if (n < 8) {  // pairwise_sum's direct loop, evaluated by every lane alike
     double r = 0.0;
@@ -396,9 +399,9 @@ __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
     return r;
   }
   if (n <= 128) return readlane_f64(pw_leaf_group(0, n, f), 0);
-  if (n <= 1928) {
+  if (n <= pw_reg_cap(RD)) {
     int my_o = 0, my_m = 0, nl = 0;
-    pw_enum_r<kPwRegDepth>(0, n, nl, lane, my_o, my_m);
+    pw_enum_r<RD>(0, n, nl, lane, my_o, my_m);
     double myval = 0.0;
     for (int b = 0; b < nl; b += 8) {
       const int l = b + (lane >> 3);
@@ -408,9 +411,9 @@ __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
       if (lane >= b && lane < b + 8) myval = moved;
     }
     int cnt = 0;
-    return pw_comb_r<kPwRegDepth>(n, cnt, myval);
+    return pw_comb_r<RD>(n, cnt, myval);
   }
-  // deeper recursion (n > 1928, P-sized sums of big configs): LDS plan
+  // deeper recursion (n > pw_reg_cap(RD), P-sized sums of big configs): LDS plan
   int nl = 1;
   if (lane == 0) S.stk[191] = pw_plan(n, S);
   wsync();
@@ -732,8 +735,7 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   L.pw.lo = reinterpret_cast<int32_t LDSP *>(base + p.off_leaf);
   L.pw.len = L.pw.lo + p.n_leaf;
   L.pw.stk = L.pw.len + p.n_leaf;
-  L.pw.acc = reinterpret_cast<double LDSP *>(base + p.off_leafval);
-  L.pw.val = L.pw.acc + 8 * p.n_leaf;
+  L.pw.val = reinterpret_cast<double LDSP *>(base + p.off_leafval);
   L.base = base;
   return L;
 }
@@ -2058,6 +2060,46 @@ __device__ __forceinline__ int block_min_int(int x, BigShared &B) {
   return s;
 }
 
+// build_bitmaps (index order) by the whole block: the words w of every
+// bitmap row are dealt to the waves, which own them through all three passes.
+// Barriers at entry (the thresholds tc / tm are written by other waves) and exit.
+__device__ __forceinline__ void big_build_bitmaps(const EnvParams &p, const Lds &L) {
+  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+  const int wid = t >> 6, nwv = NT >> 6;
+  const int P = p.P, NW = p.NW;
+  for (int i = t; i < 101 * NW; i += NT) {
+    L.bc[i] = 0;
+    L.bm[i] = 0;
+  }
+  __syncthreads();
+  for (int w = wid; w < NW; w += nwv) {
+    const int pos = w * 64 + lane;
+    if (pos < P) {
+      const int tcq = (int)L.tc[pos] - 1, tmq = (int)L.tm[pos] - 1;
+      if (tcq >= 0) __atomic_fetch_or(&L.bc[tcq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
+      if (tmq >= 0) __atomic_fetch_or(&L.bm[tmq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
+    }
+  }
+  wsync();  // the words of a wave are its own from here on
+  const int rlo = 63 - lane, rhi = 127 - lane;
+  const bool hi_ok = rhi <= 100;
+  for (int w = wid; w < NW; w += nwv) {
+    uint64_t c1 = hi_ok ? L.bc[rhi * NW + w] : 0, m1 = hi_ok ? L.bm[rhi * NW + w] : 0;
+    uint64_t c0 = L.bc[rlo * NW + w], m0 = L.bm[rlo * NW + w];
+    c1 = prefix_or64(c1);
+    m1 = prefix_or64(m1);
+    c0 = prefix_or64(c0) | readlane_u64(c1, 63);
+    m0 = prefix_or64(m0) | readlane_u64(m1, 63);
+    L.bc[rlo * NW + w] = c0;
+    L.bm[rlo * NW + w] = m0;
+    if (hi_ok) {
+      L.bc[rhi * NW + w] = c1;
+      L.bm[rhi * NW + w] = m1;
+    }
+  }
+  __syncthreads();
+}
+
 // FirstFit / BestFit act fused with the action phase (heuristic_apply, block form).
 template <int SPT>
 __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &L, const Tables &T,
@@ -2074,24 +2116,19 @@ VMP_SLOOP
   uint32_t won = 0, bad = 0;
   int64_t n_place = 0;
   if (block_sum_int(pend != 0, B) > 0) {
-    if (w0) {
-      for (int i = lane; i < P; i += 64) {
-        const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
-        L.fcpu[i] = fcv;
-        L.fmem[i] = fmv;
-        L.tc[i] = (uint8_t)(fit_threshold(fcv) + 1);
-        L.tm[i] = (uint8_t)(fit_threshold(fmv) + 1);
-      }
-      wsync();
+    for (int i = t; i < P; i += NT) {
+      const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
+      L.fcpu[i] = fcv;
+      L.fmem[i] = fmv;
+      L.tc[i] = (uint8_t)(fit_threshold(fcv) + 1);
+      L.tm[i] = (uint8_t)(fit_threshold(fmv) + 1);
     }
     bool rebuild = true;
     uint32_t hit = 0;
 #pragma unroll 1
     for (;;) {
       if (rebuild) {
-        __syncthreads();
-        if (w0) build_bitmaps(p, L, false);
-        __syncthreads();
+        big_build_bitmaps(p, L);
         hit = 0;
 VMP_SLOOP
         for (int s = 0; s < SPT; s++)
@@ -2259,108 +2296,119 @@ VMP_SLOOP
   }
 }
 
-// Wave 0 of k_env_big: the step's pairwise sums, reward, counters and
-// termination (env_tail's stats section); out of line so its temporaries do not
-// share the register budget with the block's slot arrays.
-__device__ __noinline__ void big_stats(const EnvParams &p, const Tables &T, BigShared &B,
-                                       char LDSP *base, int64_t k, int n_ex, int n_w,
-                                       int64_t n_term, int64_t arrivals) {
+// The step's pairwise sums in k_env_big (env_tail's stats section, block
+// form): job j computes res[j] with the numbers of env_tail (0,1 accepted
+// sizes; 2,3 existing VM sizes; 4,5 PM cpu / memory; 6,7 PM squared
+// deviations; 8,9 VM-size squared deviations), each by one whole wave in
+// numpy's pairwise order. Out of line so its temporaries do not share the
+// register budget with the block's slot arrays.
+constexpr int kBigPwDepth = 6;  // register plan up to n = 7688
+__device__ __noinline__ void big_sum_job(const EnvParams &p, const Tables &T, char LDSP *base,
+                                         int j, int k, int n_ex) {
+  const Lds L = make_lds(p, base);
+  const int P = p.P;
+  double LDSP *res = L.jobres;
+  const double *cent = T.cent;
+  double r;
+  if (j < 4) {
+    const uint8_t LDSP *src = (j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp);
+    r = wave_pw_sum<kBigPwDepth>(j < 2 ? k : n_ex, [=](int i) { return cent[src[i]]; }, L.pw);
+  } else if (j < 8) {
+    const double LDSP *src = (j & 1) ? L.mem : L.cpu;
+    const double mean = j < 6 ? 0.0 : res[j - 2] / (double)P;
+    const bool sq = j >= 6;
+    r = wave_pw_sum<kBigPwDepth>(P, [=](int i) {
+      const double x = src[i];
+      const double d = x - mean;
+      return sq ? d * d : x;
+    }, L.pw);
+  } else {
+    const uint8_t LDSP *src = (j & 1) ? L.mcomp : L.ccomp;
+    const double mean = res[j - 6] / (double)n_ex;
+    r = wave_pw_sum<kBigPwDepth>(n_ex, [=](int i) {
+      const double d = cent[src[i]] - mean;
+      return d * d;
+    }, L.pw);
+  }
+  wsync();
+  if (lane_id() == 0) res[j] = r;
+  wsync();
+}
+
+// The jobs of bit set `jobs` spread over the block's waves (all threads call
+// it; returns after a barrier). A sum past the register plan uses the LDS
+// plan, of which the carve holds one copy: those run on wave 0 in turn.
+__device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &T, char LDSP *base,
+                                              uint32_t jobs, int k, int n_ex) {
+  const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  int slot = 0;
+#pragma unroll 1
+  while (jobs) {
+    const int j = __builtin_ctz(jobs);
+    jobs &= jobs - 1;
+    const int n = j < 2 ? k : (j >= 4 && j < 8) ? p.P : n_ex;
+    const int w = n > pw_reg_cap(kBigPwDepth) ? 0 : (slot++ % nwv);
+    if (w == wid) big_sum_job(p, T, base, j, k, n_ex);
+  }
+  __syncthreads();
+}
+
+// Wave 0 of k_env_big after the sums: reward, counters and termination.
+__device__ __noinline__ void big_stats_final(const EnvParams &p, BigShared &B, char LDSP *base,
+                                             int64_t k, int n_ex, int n_w, int64_t n_term,
+                                             int64_t arrivals) {
   const Lds L = make_lds(p, base);
   const int lane = lane_id();
   const int P = p.P;
   const bool kl = p.reward == 2;
   EnvHdr LDSP *H = L.hdr;
+  double LDSP *res = L.jobres;
   double reward = 0.0;
-  {
-    double LDSP *res = L.jobres;
-    const double *cent = T.cent;
-    {
-#pragma unroll 1
-      for (int j = (k > 0 ? 0 : 2); j < (kl ? 4 : 2); j++) {
-        const uint8_t LDSP *src = (j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp);
-        const int n = j < 2 ? (int)k : n_ex;
-        const double r = wave_pw_sum(n, [=](int i) { return cent[src[i]]; }, L.pw);
-        wsync();
-        if (lane == 0) res[j] = r;
-        wsync();
-      }
-    }
-    if (p.reward >= 1) {
-      const int jend = p.reward == 2 ? 8 : 6;
-#pragma unroll 1
-      for (int j = 4; j < jend; j++) {
-        const double LDSP *src = (j & 1) ? L.mem : L.cpu;
-        const double mean = j < 6 ? 0.0 : res[j - 2] / (double)P;
-        const bool sq = j >= 6;
-        const double r = wave_pw_sum(P, [=](int i) {
-          const double x = src[i];
-          const double d = x - mean;
-          return sq ? d * d : x;
-        }, L.pw);
-        wsync();
-        if (lane == 0) res[j] = r;
-        wsync();
-      }
-    }
+  const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
+  const double r2 = kl ? res[2] : 0.0, r3 = kl ? res[3] : 0.0;
+  double tcm = r2 / (double)P;
+  if (p.cap_target_util && tcm > 1) tcm = 1.0;
+  double tmm = r3 / (double)P;
+  if (p.cap_target_util && tmm > 1) tmm = 1.0;
+  if (n_ex > 0) {
     if (p.reward == 2) {
-#pragma unroll 1
-      for (int j = 8; j < 10; j++) {
-        const uint8_t LDSP *src = (j & 1) ? L.mcomp : L.ccomp;
-        const double mean = res[j - 6] / (double)n_ex;
-        const double r = wave_pw_sum(n_ex, [=](int i) {
-          const double d = cent[src[i]] - mean;
-          return d * d;
-        }, L.pw);
-        wsync();
-        if (lane == 0) res[j] = r;
-        wsync();
-      }
+      double cv = res[6] / (double)P, mv = res[7] / (double)P;
+      if (cv == 0) cv = 1e-6;
+      if (mv == 0) mv = 1e-6;
+      double tcv = res[8] / (double)n_ex, tmv = res[9] / (double)n_ex;
+      if (tcv == 0) tcv = 1e-6;
+      if (tmv == 0) tmv = 1e-6;
+      reward = (tcm == 0 || tmm == 0)
+                   ? 0.0
+                   : kl_reward(tcm, tmm, tcv, tmv, res[4] / (double)P, res[5] / (double)P, cv, mv);
+    } else if (p.reward == 1) {
+      reward = p.beta * res[4] + (1 - p.beta) * res[5];
+    } else {
+      reward = -wr;
     }
-    const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
-    if (!kl) res[2] = res[3] = 0.0;
-    double tcm = res[2] / (double)P;
-    if (p.cap_target_util && tcm > 1) tcm = 1.0;
-    double tmm = res[3] / (double)P;
-    if (p.cap_target_util && tmm > 1) tmm = 1.0;
-    if (n_ex > 0) {
-      if (p.reward == 2) {
-        double cv = res[6] / (double)P, mv = res[7] / (double)P;
-        if (cv == 0) cv = 1e-6;
-        if (mv == 0) mv = 1e-6;
-        double tcv = res[8] / (double)n_ex, tmv = res[9] / (double)n_ex;
-        if (tcv == 0) tcv = 1e-6;
-        if (tmv == 0) tmv = 1e-6;
-        reward = (tcm == 0 || tmm == 0)
-                     ? 0.0
-                     : kl_reward(tcm, tmm, tcv, tmv, res[4] / (double)P, res[5] / (double)P, cv, mv);
-      } else if (p.reward == 1) {
-        reward = p.beta * res[4] + (1 - p.beta) * res[5];
-      } else {
-        reward = -wr;
-      }
-    }
-    const int64_t ts = H->timestep;
-    const bool term = ts >= p.limit;
-    wsync();
-    if (lane == 0) {
-      H->timestep = ts + 1;
-      H->total_requests += arrivals;
-      H->served += n_term;
-      H->dropped += arrivals - k;
-      H->waiting_ratio = wr;
-      if (kl) {
-        H->tcm = tcm;
-        H->tmm = tmm;
-      }
-      if (k > 0) {
-        H->total_cpu_req = H->total_cpu_req + res[0];
-        H->total_mem_req = H->total_mem_req + res[1];
-      }
-      B.b64[0] = __double_as_longlong(reward);
-      B.bc[6] = term;
-    }
-    wsync();
   }
+  const int64_t ts = H->timestep;
+  const bool term = ts >= p.limit;
+  const double a0 = k > 0 ? res[0] : 0.0, a1 = k > 0 ? res[1] : 0.0;
+  wsync();
+  if (lane == 0) {
+    H->timestep = ts + 1;
+    H->total_requests += arrivals;
+    H->served += n_term;
+    H->dropped += arrivals - k;
+    H->waiting_ratio = wr;
+    if (kl) {
+      H->tcm = tcm;
+      H->tmm = tmm;
+    }
+    if (k > 0) {
+      H->total_cpu_req = H->total_cpu_req + a0;
+      H->total_mem_req = H->total_mem_req + a1;
+    }
+    B.b64[0] = __double_as_longlong(reward);
+    B.bc[6] = term;
+  }
+  wsync();
 }
 
 __device__ __noinline__ void big_predraw(const EnvParams &p, const Tables &T, char LDSP *base,
@@ -2496,7 +2544,12 @@ VMP_SLOOP
   }
   __syncthreads();
   STAMP(11);
-  if (w0) big_stats(p, T, B, L.base, k, n_ex, n_w, n_term, arrivals);
+  {  // phase A: plain sums; phase B (kl): squared deviations about their means
+    const uint32_t ja = (k > 0 ? 0x3u : 0u) | (kl ? 0xCu : 0u) | (p.reward >= 1 ? 0x30u : 0u);
+    if (ja) big_sum_phase(p, T, L.base, ja, (int)k, n_ex);
+    if (kl) big_sum_phase(p, T, L.base, 0x3C0u, (int)k, n_ex);
+  }
+  if (w0) big_stats_final(p, B, L.base, k, n_ex, n_w, n_term, arrivals);
   __syncthreads();
   STAMP(12);
   const double reward = __longlong_as_double(B.b64[0]);
@@ -2523,16 +2576,31 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   }
   constexpr int kPoisWords = (int)(2 * sizeof(PoisConst) / 4);
   if (t < kPoisWords) reinterpret_cast<uint32_t *>(T.pois)[t] = reinterpret_cast<const uint32_t *>(p.pois)[t];
-  if (t < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[t] = reinterpret_cast<const uint64_t *>(p.hdr + e)[t];
+  // every global load of the env's state is issued before the first LDS store
+  // (indices clamped, not branched on, so the loads are unconditional):
+  // header, the first 4*NT PM words, the VM words
+  const uint64_t hv = reinterpret_cast<const uint64_t *>(p.hdr + e)[t & 31];
   const double *pm = p.pm + (int64_t)e * 2 * P;
-  for (int i = t; i < 2 * P; i += NT) L.cpu[i] = pm[i];
-  for (int i = t; i < kBigMaxSPT * kBigMaxWaves; i += NT) B.rc[i] = 0;
+  const int n_pm = 2 * P;
+  double pv[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) pv[j] = pm[min(j * NT + t, n_pm - 1)];
   const uint64_t *vmw = p.vmw + (int64_t)e * V;
+  uint64_t wv[SPT];
+#pragma unroll
+  for (int s = 0; s < SPT; s++) wv[s] = vmw[min(s * NT + t, V - 1)];
+  __asm__ volatile("" ::: "memory");
+  if (t < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[t] = hv;
+#pragma unroll
+  for (int j = 0; j < 4; j++)
+    if (j * NT + t < n_pm) L.cpu[j * NT + t] = pv[j];
+  for (int i = 4 * NT + t; i < n_pm; i += NT) L.cpu[i] = pm[i];  // P > 2 * NT
+  for (int i = t; i < kBigMaxSPT * kBigMaxWaves; i += NT) B.rc[i] = 0;
   uint32_t rem[SPT];
 #pragma unroll
-  for (int s = 0; s < SPT; s++) {  // all loads in flight at once; rem[] in registers
+  for (int s = 0; s < SPT; s++) {  // rem[] statically indexed: stays in registers
     const int v = s * NT + t;
-    const uint64_t w = v < V ? vmw[v] : (uint64_t)kPad;
+    const uint64_t w = v < V ? wv[s] : (uint64_t)kPad;
     W[v] = (uint32_t)w;
     rem[s] = (uint32_t)(w >> 32);
   }

@@ -66,10 +66,14 @@ class Base:
 
     def test(self, show: bool = False, output: str = None, debug: bool = False):
         """base.py:63-118: one eval episode (eval_steps) from reset(seed=config.seed),
-        every step recorded; returns the Record (saved to `output` if given)."""
+        every step recorded; returns the Record (saved to `output` if given). The
+        Record metrics are accumulated on the device during the episode
+        (vmp_record_*); the host keeps the per-step traces of the JSON."""
         self.env.eval()
         self.eval()
         obs, info = self.env.reset(seed=self.env.config.seed)
+        dev = batched_env(self.env)
+        dev.record(True)  # right after reset, as base.py:67-71 records from there
         done = False
         while not done:
             if debug:
@@ -82,6 +86,8 @@ class Base:
                 print("reward: \t\t%.2f" % (reward))
                 print("")
             self.record_testing_step(reward, info)
+        self.record.set_device_summary(dev.record_summary()[0])
+        dev.record(False)
         summary = self.record.get_summary()
         if show:
             print(self.env.config)

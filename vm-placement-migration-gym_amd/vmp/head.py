@@ -63,6 +63,18 @@ class HeadRng:
         self.offset = 0
         self.counter = None
 
+    def fold(self, k):
+        """Give stream k (e.g. a data-parallel rank) its own seed: splitmix64 of
+        seed ^ k * golden ratio. Stream 0 keeps the seed, so rank 0 of a job draws
+        what a single process would."""
+        if k:
+            z = (self.seed ^ (int(k) * 0x9E3779B97F4A7C15)) & (2**64 - 1)
+            z = (z + 0x9E3779B97F4A7C15) & (2**64 - 1)
+            z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+            z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+            self.seed = z ^ (z >> 31)
+        return self
+
     def graph_counter(self, device):
         if self.counter is None:
             self.counter = torch.zeros(1, dtype=torch.int64, device=device)

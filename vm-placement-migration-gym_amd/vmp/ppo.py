@@ -350,6 +350,12 @@ class PPOTrainer:
         self.ep_t = 0
         self.ep_returns = []
         self.stats = {}
+        if self.dist and not getattr(self.model.rng, "rank_folded", False):
+            # every rank seeds torch alike (same initial parameters): its sampling
+            # stream must still differ, or env b of every rank draws the same
+            # uniforms and the global batch is correlated across ranks
+            self.model.rng.fold(self.rank)
+            self.model.rng.rank_folded = True
         if self.dist and allocate:
             self._sync_params()
         if allocate:

@@ -1,151 +1,81 @@
-"""Record: per-step evaluation metrics of Base.test, field for field the
-reference's src/record.py:5-160 (same attribute names, summary keys and JSON
-layout, so plots.ipynb and the exp_* drivers read our files unchanged)."""
+"""Record (src/record.py:5-176) for the MI355X env.
+
+The reference derives every evaluation metric on the host from per-step lists
+(record.py:34-134: splitting each slot's placement history at its arrival
+steps, then pending / slowdown / lifetime per VM life). Here those metrics are
+accumulated on the device while the episode runs (vmp_record_enable /
+vmp_record_read, csrc/vmp_record.hip) and `summary_from_device` turns the
+recorder's sums and rate histograms into get_summary()'s dict. `Record` keeps
+the reference's attribute names for the per-step traces Base.test appends, so
+save() writes the JSON layout plots.ipynb and the exp_* drivers read, and its
+summary is the device one. (The literal host restatement of record.py lives in
+tests/record_literal.py, where it checks the device recorder.)
+"""
 import json
 import os
 
 import numpy as np
 
+# Record.get_summary keys in the reference's order (record.py:110-134)
+SUMMARY_KEYS = (
+    "total rewards", "total served VMs", "total requests", "total cpu requested",
+    "total memory requested", "total suspend actions", "total place actions", "average VM life",
+    "average pending", "median pending", "max pending", "average slowdown", "median slowdown",
+    "max slowdown", "drop rate", "cpu mean", "cpu mean target", "cpu std", "memory mean",
+    "memory mean target", "memory std", "rank mean")
+TRACE_KEYS = ("cpu", "memory", "used_pm", "vm_placements", "waiting_ratio", "actions", "rewards",
+              "dropped_requests", "total_requests", "vm_arrival_steps", "target_cpu_mean",
+              "target_memory_mean", "served_requests", "total_cpu_requested",
+              "total_memory_requested", "suspended", "placed", "vmsratio", "rank")
+
 
 class Record:
+    """Per-step traces (same attributes as record.py:7-31) + the device summary."""
+
     def __init__(self, agent, env_config, agent_config):
         self.agent = agent
         self.env_config = env_config if isinstance(env_config, dict) else vars(env_config)
         self.agent_config = agent_config if isinstance(agent_config, dict) else None
         self.WAIT_STATUS = self.env_config["pms"]
-        self.cpu = []
-        self.memory = []
-        self.used_pm = []
-        self.vm_placements = []
-        self.waiting_ratio = []
-        self.actions = []
-        self.rewards = []
-        self.dropped_requests = []
-        self.total_requests = []
-        self.vm_arrival_steps = []
-        self.target_cpu_mean = []
-        self.target_memory_mean = []
-        self.served_requests = []
-        self.total_cpu_requested = []
-        self.total_memory_requested = []
-        self.suspended = []
-        self.placed = []
-        self.vmsratio = []
-        self.rank = []
+        for k in TRACE_KEYS:
+            setattr(self, k, [])
+        self._device = None  # summary_from_device(...) of the recorded episode
 
-    # record.py:33-51: split each slot's placement history at its arrival steps
-    @property
-    def unique_vms_placement(self):
-        out = []
-        vm_placements = np.transpose(np.array(self.vm_placements))
-        for vm, vm_status in enumerate(vm_placements):
-            if len(self.vm_arrival_steps[vm]) == 0:
-                continue
-            start = 0
-            for end in self.vm_arrival_steps[vm][1:]:
-                end -= 2  # vm_placements starts from timestep 2
-                seg = vm_status[start:end]
-                out.append(seg[seg <= self.WAIT_STATUS])
-                start = end
-            seg = vm_status[start:]
-            assert seg[seg <= self.WAIT_STATUS].size != 0, seg[seg <= self.WAIT_STATUS]
-            out.append(seg[seg <= self.WAIT_STATUS])
-        return out
-
-    def _first_run(self, status):
-        running = np.where(status < self.WAIT_STATUS)[0]
-        return running[0] if running.size > 0 else None
+    def set_device_summary(self, summary):
+        """Attach the recorder's summary of the episode (Base.test does this)."""
+        self._device = dict(summary)
 
     @property
-    def pending_rates(self):  # record.py:53-65 (allocated_at == 0 counts as "never", as there)
-        rates = []
-        for status in self.unique_vms_placement:
-            status = np.array(status)
-            at = self._first_run(status)
-            rates.append(np.around((at + 1.0) / len(status), 3) if at else 1.0)
-        return rates
+    def device_summary(self):
+        """summary_from_device's full dict (incl. the unrounded `_` columns)."""
+        return self._device
 
-    @property
-    def slowdown_rates(self):  # record.py:67-82
-        rates = []
-        for status in self.unique_vms_placement:
-            status = np.array(status)
-            at = self._first_run(status)
-            if at:
-                slow = np.count_nonzero(status[at:] == self.WAIT_STATUS)
-                life = len(status) - at - 1
-                rates.append(0 if life == 0 else np.around(slow / life, 3))
-        return rates if rates else [0]
-
-    @property
-    def vm_lifetime(self):  # record.py:84-95
-        life = []
-        for status in self.unique_vms_placement:
-            status = np.array(status)
-            at = self._first_run(status)
-            life.append(len(status) - at - 1 if at else 0)
-        return life
-
-    @property
-    def drop_rate(self):
-        dropped = np.array(self.dropped_requests)
-        total = np.array(self.total_requests)
-        return np.divide(dropped, total, out=np.zeros(dropped.shape, dtype=float),
-                         where=total != 0)
-
-    @property
-    def total_rewards(self):
-        rewards = np.array(self.rewards)
-        rewards[rewards < -1e7] = np.mean(rewards[rewards > -1e7])
-        return np.round(np.sum(rewards), 3)
-
-    def get_summary(self):  # record.py:110-133, same keys and rounding
-        pend = self.pending_rates
-        slow = self.slowdown_rates
-        return {
-            "total rewards": self.total_rewards,
-            "total served VMs": self.served_requests[-1],
-            "total requests": self.total_requests[-1],
-            "total cpu requested": np.round(self.total_cpu_requested, 3),
-            "total memory requested": np.round(self.total_memory_requested, 3),
-            "total suspend actions": self.suspended[-1],
-            "total place actions": self.placed[-1],
-            "average VM life": np.round(np.mean(self.vm_lifetime), 3),
-            "average pending": np.round(np.mean(pend), 3),
-            "median pending": np.round(np.median(pend), 3),
-            "max pending": np.round(np.max(pend), 3) if len(pend) > 0 else 0,
-            "average slowdown": np.round(np.mean(slow), 3),
-            "median slowdown": np.round(np.median(slow), 3),
-            "max slowdown": np.round(np.max(slow), 3),
-            "drop rate": np.round(np.mean(self.drop_rate), 3),
-            "cpu mean": np.round(np.mean(self.cpu), 3),
-            "cpu mean target": np.round(np.mean(self.target_cpu_mean), 3),
-            "cpu std": np.round(np.std(self.cpu), 3),
-            "memory mean": np.round(np.mean(self.memory), 3),
-            "memory mean target": np.round(np.mean(self.target_memory_mean), 3),
-            "memory std": np.round(np.std(self.memory), 3),
-            "rank mean": np.round(np.mean(self.rank), 3),
-        }
+    def get_summary(self):
+        """record.py:110-134: same keys, same rounding; values from the device."""
+        if self._device is None:
+            raise RuntimeError("no recorded episode: run Base.test on the GPU env (the metrics "
+                               "are accumulated on the device) or import a saved record")
+        return {k: self._device[k] for k in SUMMARY_KEYS}
 
     def save(self, path: str):
+        """record.py:136-142: vars(self) as JSON, incl. `summary`."""
         self.summary = self.get_summary()
         parent = os.path.dirname(path)
         if parent:
             os.makedirs(parent, exist_ok=True)
+        out = {k: v for k, v in vars(self).items() if k != "_device"}
         with open(path, "w") as f:
-            f.write(json.dumps(vars(self), cls=NpEncoder))
+            f.write(json.dumps(out, cls=NpEncoder))
 
     @classmethod
-    def import_record(cls, agent: str, jsondict: dict):  # record.py:144-168
-        r = cls(agent, jsondict["env_config"], jsondict["agent_config"])
-        for k in ("cpu", "memory", "vm_placements", "waiting_ratio", "actions", "rewards",
-                  "total_requests", "dropped_requests", "vm_arrival_steps", "target_cpu_mean",
-                  "target_memory_mean", "served_requests", "total_cpu_requested",
-                  "total_memory_requested", "rank", "suspended"):
-            setattr(r, k, jsondict[k])
-        for k in ("used_pm", "placed"):
+    def import_record(cls, agent: str, jsondict: dict):
+        """record.py:144-168: the traces of a saved record, and its saved summary."""
+        r = cls(agent, jsondict["env_config"], jsondict.get("agent_config"))
+        for k in TRACE_KEYS:
             if k in jsondict:
                 setattr(r, k, jsondict[k])
+        if "summary" in jsondict:
+            r.set_device_summary(jsondict["summary"])
         return r
 
 
