@@ -169,8 +169,8 @@ def main():
 
     # ---- replica reduction: counters summed, per-env returns of the
     # last fused rollout gathered over ranks (RCCL at N > 1) ----
-    from vmp.replicas import reduce_replicas
-    ctr_sum, ret_all = reduce_replicas(env.counters(), rbuf.sum(0), dist)
+    from vmp.replicas import reduce_replicas, step_returns
+    ctr_sum, ret_all = reduce_replicas(env.counters(), step_returns(rbuf), dist)
     replicas = {"counters_sum": [int(x) for x in ctr_sum.cpu().tolist()],
                 "counters": ["total_requests", "served", "suspend_action", "place_action",
                              "dropped", "timestep"],

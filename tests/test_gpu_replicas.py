@@ -28,10 +28,10 @@ def _free_port():
 def _run(rank, n_local, dist=None):
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
-    from vmp.replicas import reduce_replicas, shard_seeds
+    from vmp.replicas import reduce_replicas, shard_seeds, step_returns
     env = BatchedVmEnv(Config(**CFG), n_local, seeds=shard_seeds(rank, n_local), device="cuda:0")
     rs, _ = env.rollout("firstfit", K)
-    out = reduce_replicas(env.counters().cpu(), rs.sum(0).cpu(), dist)
+    out = reduce_replicas(env.counters().cpu(), step_returns(rs).cpu(), dist)
     env.close()
     return out
 

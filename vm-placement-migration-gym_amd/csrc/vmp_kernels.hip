@@ -405,7 +405,10 @@ __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
     double myval = 0.0;
     for (int b = 0; b < nl; b += 8) {
       const int l = b + (lane >> 3);
-      const int o = __shfl(my_o, l & 63), m = l < nl ? __shfl(my_m, l & 63) : 0;
+      // both shuffles unconditional: a ds_bpermute under a partial exec mask
+      // must not read a source lane that the mask left out
+      const int o = __shfl(my_o, l & 63), m_src = __shfl(my_m, l & 63);
+      const int m = l < nl ? m_src : 0;
       const double v = pw_leaf_group(o, m, f);
       const double moved = __shfl(v, ((lane - b) & 7) * 8);
       if (lane >= b && lane < b + 8) myval = moved;

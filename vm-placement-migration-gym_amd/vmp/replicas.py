@@ -18,6 +18,16 @@ def shard_seeds(rank, n_local, base=0, stride=4):
     return base + stride * (int(rank) * int(n_local) + np.arange(int(n_local), dtype=np.int64))
 
 
+def step_returns(rewards):
+    """Per-env sum of a [K, n] reward block in step order (k = 0, 1, ...):
+    elementwise adds, so an env's return does not depend on how many envs share
+    its launch (a torch reduction over dim 0 may block differently per shape)."""
+    ret = rewards[0].clone()
+    for k in range(1, rewards.shape[0]):
+        ret += rewards[k]
+    return ret
+
+
 def reduce_replicas(counters, returns, dist=None):
     """counters int64 [n_local, C], returns float [n_local] (this rank's envs) ->
     (counter sums int64 [C] over all envs of the job, returns [world * n_local]
