@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=512)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--ff", type=int, default=200)
+    ap.add_argument("--ff", type=int, default=2000)
     ap.add_argument("--policy", default="bestfit")
     ap.add_argument("--reward", default="kl")
     args = ap.parse_args()
@@ -35,8 +35,8 @@ def main():
     t0 = time.perf_counter()
     left = args.ff
     while left > 0:
-        env.rollout(args.policy, min(50, left))
-        left -= 50
+        env.rollout(args.policy, min(250, left))
+        left -= 250
     torch.cuda.synchronize()
     ff_s = time.perf_counter() - t0
     dev = env.device

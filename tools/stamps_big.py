@@ -23,8 +23,8 @@ cfg = Config(pms=P, vms=V, arrival_rate=round(1000 / 0.55 / 1000, 3), service_le
 env = BatchedVmEnv(cfg, N, seeds=4 * np.arange(N, dtype=np.int64), device="cuda:0")
 left = FF
 while left > 0:
-    env.rollout(POL, min(50, left))
-    left -= 50
+    env.rollout(POL, min(250, left))
+    left -= 250
 NS = 24
 buf = torch.zeros((N, NS), dtype=torch.int64, device="cuda")
 _lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
@@ -39,9 +39,10 @@ torch.cuda.synchronize()
 _lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
 torch.cuda.synchronize()
 st = buf.cpu().numpy().astype(np.float64) / K
-names = {13: "pro:load", 14: "pro:predraw", 17: "heur:rebuild+query", 18: "heur:min+pick",
+names = {13: "pro:load+predraw", 22: "heur:bitmaps", 17: "heur:query", 18: "heur:min+pick",
          19: "heur:choose+place(w0)", 16: "heur:rest", 2: "run_vms", 3: "accept",
-         11: "stats:rank+compact", 12: "stats:big_stats(w0)", 4: "tail-rest", 6: "obs+store"}
+         11: "stats:rank+compact", 20: "stats:phase A (+obs)", 21: "stats:phase B",
+         12: "stats:final", 4: "tail-rest", 6: "obs+store"}
 tot = st.sum(1)
 pl = env.state()["vm_placement"].cpu().numpy()
 print(f"N={N} ff={FF} policy={POL}: {ev0.elapsed_time(ev1) / K:.3f} ms/step, mean cycles per "

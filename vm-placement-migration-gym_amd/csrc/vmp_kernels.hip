@@ -871,6 +871,18 @@ __device__ __forceinline__ int bm_query(const Lds &L, int NW, int kc, int km) {
   return -1;
 }
 
+// Does any visiting position accept sizes (kc, km)? No early exit, so the
+// row reads of all words are in flight together (latency of one LDS round trip
+// per 8 words instead of one per word).
+__device__ __forceinline__ bool bm_any(const Lds &L, int NW, int kc, int km) {
+  const uint64_t LDSP *rc = L.bc + kc * NW;
+  const uint64_t LDSP *rm = L.bm + km * NW;
+  uint64_t acc = 0;
+#pragma unroll 8
+  for (int w = 0; w < NW; w++) acc |= rc[w] & rm[w];
+  return acc != 0;
+}
+
 // BestFit's choice for sizes (kc, km) (bestfit.py:33-39): the first PM in
 // visiting order flip(argsort(fcpu + fmem)) that fits, i.e. the fitting PM of
 // largest key. Fast path: a wave argmax over the PMs; only when two or more
@@ -2132,6 +2144,7 @@ VMP_SLOOP
     for (;;) {
       if (rebuild) {
         big_build_bitmaps(p, L);
+        STAMP(22);
         hit = 0;
 VMP_SLOOP
         for (int s = 0; s < SPT; s++)
@@ -2214,7 +2227,7 @@ VMP_SLOOP
           if (!((hit >> s) & 1u)) continue;
           const uint32_t w = W[s * NT + t];
           const int c = w_cc(w), m = w_cm(w);
-          if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && bm_query(L, NW, c, m) < 0)
+          if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && !bm_any(L, NW, c, m))
             hit &= ~(1u << s);
         }
       }
@@ -2421,12 +2434,68 @@ __device__ __noinline__ void big_predraw(const EnvParams &p, const Tables &T, ch
   predraw(p, L, T, K, p.V, JA, JM);
 }
 
+// The env's outputs of the launch that are final once the step's accept
+// phase is done: obs (VM part and PM part, env.py:295-296) and, with `state`,
+// the VM words and PM resources. Issued before the stats so the stores drain
+// while the pairwise sums run (the header follows at the end of the launch).
+template <int SPT>
+__device__ __forceinline__ void big_store(const EnvParams &p, const Lds &L, const Tables &T,
+                                          const uint32_t LDSP *W, const uint32_t (&rem)[SPT],
+                                          float *obs, bool state, int e) {
+  const int t = threadIdx.x, NT = blockDim.x;
+  const int V = p.V, P = p.P;
+  uint64_t *vmo = p.vmw + (int64_t)e * V;
+#pragma unroll
+  for (int s = 0; s < SPT; s++) {  // rem[] statically indexed
+    const int v = s * NT + t;
+    const uint32_t w = W[v];
+    if (live(w)) {
+      if (obs) {
+        ST_NT(obs + v, (float)w_pl(w));
+        ST_NT(obs + V + v, T.fcent[w_cc(w)]);
+        ST_NT(obs + 2 * V + v, T.fcent[w_cm(w)]);
+      }
+      if (state) ST_NT(vmo + v, (uint64_t)w | ((uint64_t)rem[s] << 32));
+    }
+  }
+  if (obs)
+    for (int i = t; i < P; i += NT) {
+      ST_NT(obs + 3 * V + i, (float)L.cpu[i]);
+      ST_NT(obs + 3 * V + P + i, (float)L.mem[i]);
+    }
+  if (state) {
+    double *pmo = p.pm + (int64_t)e * 2 * P;
+    for (int i = t; i < 2 * P; i += NT) ST_NT(pmo + i, (double)L.cpu[i]);
+  }
+}
+
+// obs (env.py:295-296) from the LDS state by the threads [0, n) of a subset
+// of the block's waves (thread i of them: slots i, i + n, ...).
+__device__ __forceinline__ void big_store_obs(const EnvParams &p, const Lds &L, const Tables &T,
+                                              const uint32_t LDSP *W, float *obs, int i, int n) {
+  const int V = p.V, P = p.P;
+#pragma unroll 4
+  for (int v = i; v < V; v += n) {
+    const uint32_t w = W[v];
+    ST_NT(obs + v, (float)w_pl(w));
+    ST_NT(obs + V + v, T.fcent[w_cc(w)]);
+    ST_NT(obs + 2 * V + v, T.fcent[w_cm(w)]);
+  }
+  for (int q = i; q < P; q += n) {
+    ST_NT(obs + 3 * V + q, (float)L.cpu[q]);
+    ST_NT(obs + 3 * V + P + q, (float)L.mem[q]);
+  }
+}
+
 // _run_vms, _accept_vm_requests, stats + reward, termination (env_tail, block form).
+// out_obs / store_state: big_store right after the accept phase (last step of
+// the launch only).
 template <int SPT>
 __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, const Tables &T,
                                            BigShared &B, uint32_t LDSP *W,
                                            uint32_t (&rem)[SPT], int kstep,
-                                           bool &terminated STAMP_PARAMS) {
+                                           bool &terminated, float *out_obs, bool store_state,
+                                           int e STAMP_PARAMS) {
   const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
@@ -2520,6 +2589,8 @@ VMP_SLOOP
     }
   }
   __syncthreads();
+  // the VM words and PM resources are final: their owners store them now
+  if (store_state) big_store<SPT>(p, L, T, W, rem, nullptr, true, e);
   STAMP(3);
   // ---- stats + reward ----
   const bool kl = p.reward == 2;
@@ -2549,8 +2620,17 @@ VMP_SLOOP
   STAMP(11);
   {  // phase A: plain sums; phase B (kl): squared deviations about their means
     const uint32_t ja = (k > 0 ? 0x3u : 0u) | (kl ? 0xCu : 0u) | (p.reward >= 1 ? 0x30u : 0u);
+    // the observation is written by the waves that get no phase-A sum (job i
+    // runs on wave i), so its stores drain while the sums run
+    const int nwv = NT >> 6, nj = __popc(ja);
+    if (out_obs) {
+      const int ws = nj < nwv ? nj : 0;
+      if ((t >> 6) >= ws) big_store_obs(p, L, T, W, out_obs, t - 64 * ws, NT - 64 * ws);
+    }
     if (ja) big_sum_phase(p, T, L.base, ja, (int)k, n_ex);
+    STAMP(20);
     if (kl) big_sum_phase(p, T, L.base, 0x3C0u, (int)k, n_ex);
+    STAMP(21);
   }
   if (w0) big_stats_final(p, B, L.base, k, n_ex, n_w, n_term, arrivals);
   __syncthreads();
@@ -2594,6 +2674,12 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   for (int s = 0; s < SPT; s++) wv[s] = vmw[min(s * NT + t, V - 1)];
   __asm__ volatile("" ::: "memory");
   if (t < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[t] = hv;
+  // the random draws need only the header: wave 0 takes them while its own
+  // PM / VM loads are still in flight
+  if (o.k_steps > 0 && w0) {
+    wsync();
+    big_predraw(p, T, L.base, o.k_steps, p.jump + 4 * lane);
+  }
 #pragma unroll
   for (int j = 0; j < 4; j++)
     if (j * NT + t < n_pm) L.cpu[j * NT + t] = pv[j];
@@ -2609,12 +2695,6 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   }
   __syncthreads();
   STAMP(13);
-  if (o.k_steps > 0 && w0) {
-    const uint64_t *jt = p.jump + 4 * lane;
-    big_predraw(p, T, L.base, o.k_steps, jt);
-  }
-  __syncthreads();
-  STAMP(14);
   bool term = false;
   int64_t ndone = 0;
 #pragma unroll 1
@@ -2634,7 +2714,9 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
       L.hdr->suspend_action += n_susp;
     }
     __syncthreads();
-    const double r = big_tail<SPT>(p, L, T, B, W, rem, k, term STAMP_ARGS);
+    const double r = big_tail<SPT>(p, L, T, B, W, rem, k, term,
+                                   last && o.obs ? o.obs + (int64_t)e * p.D : nullptr, last, e
+                                   STAMP_ARGS);
     if (o.reward && t == 0) o.reward[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
@@ -2648,23 +2730,8 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   }
   __syncthreads();
   STAMP(4);
-  if (o.obs) {
-    float *obs = o.obs + (int64_t)e * p.D;
-VMP_SLOOP
-    for (int s = 0; s < SPT; s++) {
-      const int v = s * NT + t;
-      const uint32_t w = W[v];
-      if (live(w)) {
-        ST_NT(obs + v, (float)w_pl(w));
-        ST_NT(obs + V + v, T.fcent[w_cc(w)]);
-        ST_NT(obs + 2 * V + v, T.fcent[w_cm(w)]);
-      }
-    }
-    for (int i = t; i < P; i += NT) {
-      ST_NT(obs + 3 * V + i, (float)L.cpu[i]);
-      ST_NT(obs + 3 * V + P + i, (float)L.mem[i]);
-    }
-  }
+  // a stepping launch stored obs and state after its last accept phase
+  if (o.obs && o.k_steps == 0) big_store<SPT>(p, L, T, W, rem, o.obs + (int64_t)e * p.D, false, e);
   if (o.mask_bits) {
     uint32_t *bits = o.mask_bits + (int64_t)e * V * p.W32;
     const int A = p.A, NW32 = p.W32, WAIT = p.P, NUL = p.P + 1;
@@ -2697,15 +2764,6 @@ VMP_SLOOP
   if (o.k_steps > 0) {
     if (o.done && t == 0) o.done[e] = (uint8_t)term;
     if (o.done_count && t == 0) o.done_count[e] += ndone;
-    uint64_t *vmo = p.vmw + (int64_t)e * V;
-#pragma unroll
-    for (int s = 0; s < SPT; s++) {
-      const int v = s * NT + t;
-      const uint32_t w = W[v];
-      if (live(w)) ST_NT(vmo + v, (uint64_t)w | ((uint64_t)rem[s] << 32));
-    }
-    double *pmo = p.pm + (int64_t)e * 2 * P;
-    for (int i = t; i < 2 * P; i += NT) ST_NT(pmo + i, (double)L.cpu[i]);
     if (t < 32)
       reinterpret_cast<uint64_t *>(p.hdr + e)[t] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
   }
