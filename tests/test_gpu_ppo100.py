@@ -1,0 +1,108 @@
+"""BASELINE config 3 pinned on the MI355X: PPO at the config/100.yml shape
+(P100 / V300, A = 102, D = 1100; hidden 512, batch 100 / minibatch 25,
+reward wr), src/agents/ppo.py:172-295.
+
+  - the reference's update() at this shape (tests/golden/ppo100_update.npz,
+    tools/gen_golden.py gen_ppo100: hidden 8, the reference's own sampled
+    batch, 2 and 4 epochs) through the HIP head and GAE;
+  - PPOTrainer on 64 GPU envs: the sampled action streams of 4 envs replayed
+    through the C oracle are bit-exact on masks, observations, f64->f32
+    rewards and counters (App. C item 4); every sampled action is valid under
+    its mask; the update equals the same trainer with the plain-PyTorch
+    reference head and GAE (tests/torch_ref.py) within 1e-5 relative."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.torch_ref import torch_gae, torch_head, unpack_bits
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+CFG100 = dict(pms=100, vms=300, service_length=1000, arrival_rate=1.8182, training_steps=10000,
+              eval_steps=100000, seed=0, reward_function="wr", sequence="uniform",
+              cap_target_util=True, beta=0.5, allow_null_action=True)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+
+
+@pytest.mark.parametrize("k_epochs", [2, 4])
+def test_update_matches_reference_100yml_on_gpu(k_epochs):
+    """PPOAgent.update (ppo.py:229-295) at the 100.yml shape through the HIP head
+    and GAE against the reference's (tests/test_ppo_cpu.py ppo100_check: 2
+    epochs within 2e-6; 4 epochs the same minibatch / KL-break sequence and 5 %
+    of the update)."""
+    from tests.test_ppo_cpu import _ppo100_update, ppo100_check
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import PPOAgent, PPOConfig
+    env = BatchedVmEnv(Config(**CFG100), 1, device=DEV)
+    ag = PPOAgent(env, PPOConfig(hidden_size=8, episodes=1, batch_size=100, minibatch_size=25,
+                                 migration_ratio=0.002, k_epochs=k_epochs))
+    d, ag, st = _ppo100_update(k_epochs, agent=ag)
+    ppo100_check(d, ag.model, st, k_epochs, atol_e2=2e-6)
+    env.close()
+
+
+def test_trainer_100yml_replay_validity_and_reference_update():
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import PPOAgent, PPOConfig, PPOTrainer
+    N, V, A, P = 64, 300, 102, 100
+    torch.manual_seed(0)
+    env = BatchedVmEnv(Config(**CFG100), N, device=DEV)
+    pcfg = dict(hidden_size=512, batch_size=100, minibatch_size=25, migration_ratio=0.002,
+                masked=True)
+    ag = PPOAgent(env, PPOConfig(**pcfg))
+    p0 = {k: v.clone() for k, v in ag.model.state_dict().items()}
+    tr = ag.trainer()
+    tr.collect()
+    T = tr.T
+    # (b) every sampled action is valid under its mask (no row is all masked:
+    # allow_null_action keeps NULL rows valid, env.py:26, 36-42)
+    bits = tr.bits.reshape(T * N, V, -1)
+    full = unpack_bits(bits, A).reshape(T, N, V, A)
+    assert not full.gather(-1, tr.act.long()[..., None]).any()
+    # (a) replay the sampled streams of 4 envs through the oracle, bit-exact
+    ctr = env.counters().cpu().numpy()
+    for i in (0, 1, 31, 63):
+        seed = int(CFG100["seed"]) + 4 * i  # PPOTrainer._episode_seeds, episode 0
+        e = O.OracleEnv(dict(CFG100, seed=seed))
+        e.eval(False)
+        e.reset(seed)
+        acts = tr.act[:, i].cpu().numpy().astype(np.int64)
+        obs = tr.obs[:, i].cpu().numpy()
+        m = full[:, i].cpu().numpy()
+        rew = tr.rew[:, i].cpu().numpy()
+        for t in range(T):
+            assert np.array_equal(e.obs(), obs[t]), (i, t)
+            assert np.array_equal(e.mask(), m[t]), (i, t)
+            o, r, _, _ = e.step(acts[t])
+            assert np.float32(r) == rew[t], (i, t, r, rew[t])
+        assert np.array_equal(o, tr.last_obs[i].cpu().numpy()), i
+        assert np.array_equal(e.counters()[0], ctr[i]), i
+    # (c) the update = the same trainer with the torch reference head and GAE
+    with torch.no_grad():
+        values = tr._values(tr.obs)
+        nv = torch.empty_like(values)
+        nv[:-1] = values[1:]
+        nv[-1] = tr._values(tr.last_obs[None])[0]
+    bufs = [x.clone() for x in (tr.obs, tr.bits, tr.act, tr.logp, tr.rew, tr.done)]
+    st = tr.update_from(*bufs, values, nv)
+    ref = PPOAgent(env, PPOConfig(**pcfg), head=torch_head, gae=torch_gae)
+    ref.model.load_state_dict(p0)
+    st_r = PPOTrainer(ref, allocate=False, distributed=False).update_from(*bufs, values, nv)
+    assert st["minibatches"] == st_r["minibatches"] and st["kl_breaks"] == st_r["kl_breaks"]
+    for k, v in ag.model.state_dict().items():
+        r = ref.model.state_dict()[k]
+        assert not torch.equal(v, p0[k]), k
+        torch.testing.assert_close(v, r, rtol=1e-5, atol=1e-6, msg=k)
+    env.close()

@@ -314,8 +314,80 @@ def gen_ppo():
           max(float(np.abs(after[k] - before[k]).max()) for k in before))
 
 
+def gen_ppo100():
+    """One reference PPOAgent.update() at the config/100.yml shape (P100 / V300,
+    A 102, D 1100; BASELINE config 3) on a 100-step batch the reference's own
+    model sampled from its env, at hidden size 8 so the fixture stays small.
+    Masks are stored bit-packed (np.packbits over the [V, A] rows)."""
+    from src.agents.ppo import PPOAgent, PPOConfig
+    torch.manual_seed(0)
+    np.random.seed(0)
+    c = dict(BASE, pms=100, vms=300, service_length=1000, arrival_rate=1.8182,
+             training_steps=10000, eval_steps=100000, seed=0, reward_function="wr",
+             cap_target_util=True, allow_null_action=True)
+    env = make_env(c, "wr")
+    agent = PPOAgent(env, PPOConfig(hidden_size=8, episodes=1, batch_size=100,
+                                    minibatch_size=25, migration_ratio=0.002,
+                                    training_progress_bar=False))
+    model = agent.model
+    before = {k: v.detach().clone().numpy() for k, v in model.state_dict().items()}
+    B = agent.config.batch_size
+    V, A, D = env.config.vms, env.action_dim, agent.obs_dim
+    masks = torch.zeros((B, V, A), dtype=bool)
+    acts = torch.zeros((B, V), dtype=int)
+    obs_b, nobs_b = torch.zeros(B, D), torch.zeros(B, D)
+    lp_b, r_b = torch.zeros(B), torch.zeros(B)
+    d_b = torch.zeros(B, dtype=int)
+    obs, _ = env.reset(seed=3)
+    obs = torch.tensor(obs)
+    for i in range(B):
+        m = torch.tensor(env.get_invalid_action_mask(True))
+        with torch.no_grad():
+            a, lp, _ = model.get_action(obs[None], invalid_mask=m)
+        a = a.flatten()
+        nobs, r, d, _, _ = env.step(a.numpy())
+        nobs = torch.tensor(nobs)
+        masks[i], acts[i], obs_b[i], nobs_b[i] = m, a, obs, nobs
+        lp_b[i], r_b[i], d_b[i] = lp.item(), r, int(i == 60)
+        obs = nobs
+    out = {"b_mask_bits": np.packbits(masks.numpy().reshape(B, -1), axis=1),
+           "b_action": acts.numpy().astype(np.int16), "b_obs": obs_b.numpy(),
+           "b_next_obs": nobs_b.numpy(), "b_logprob": lp_b.numpy(), "b_reward": r_b.numpy(),
+           "b_done": d_b.numpy(), "shape": np.array([B, V, A, D])}
+    # k_epochs = 2 (8 AdamW steps, every ratio stays inside the clip range) and
+    # the config's 4 epochs (the reference breaks on KL in epoch 4): counted
+    # head calls and optimizer steps record where its minibatch loop stopped
+    args = (masks, acts, obs_b, nobs_b, lp_b, r_b, d_b)
+    for tag, ke in (("e2_", 2), ("", 4)):
+        model.load_state_dict({k: torch.tensor(v) for k, v in before.items()})
+        agent.config.k_epochs = ke
+        agent.optimizer = torch.optim.AdamW(model.parameters(), lr=agent.config.lr)
+        n = {"head": 0, "step": 0}
+        ga, st = model.get_action, agent.optimizer.step
+
+        def get_action(*a, **k):
+            n["head"] += 1
+            return ga(*a, **k)
+
+        def step(*a, **k):
+            n["step"] += 1
+            return st(*a, **k)
+        model.get_action, agent.optimizer.step = get_action, step
+        agent.update(*[x.clone() for x in args])
+        model.get_action = ga
+        after = {k: v.detach().clone().numpy() for k, v in model.state_dict().items()}
+        out.update({"p1_" + tag + k: v for k, v in after.items()})
+        out[tag + "ref_calls"] = np.array([n["head"], n["step"]])
+    out.update({"p0_" + k: v for k, v in before.items()})
+    np.savez_compressed(os.path.join(OUT, "ppo100_update.npz"), **out)
+    print("ppo100 update done; max |dp| =",
+          max(float(np.abs(after[k] - before[k]).max()) for k in before))
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["rng", "traj", "ppo"]
+    what = sys.argv[1:] or ["rng", "traj", "ppo", "ppo100"]
+    if "ppo100" in what:
+        gen_ppo100()
     if "rng" in what:
         gen_rng_kat()
     if "traj" in what:
