@@ -294,32 +294,33 @@ __global__ __launch_bounds__(256) void k_head_bwd(HeadArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Tiled row kernels (A <= kTileMaxA, the 10.yml / 100.yml shapes): one wave
-// per tile of 64 consecutive (b, v) rows, lane = row. The tile (64*A floats,
-// contiguous in HBM) is copied into LDS with 16-B loads (fully coalesced,
-// every byte read once), then each lane runs its row out of LDS (even A:
-// 8-B ds_read_b64 row reads, conflict-free for A = 102). Row statistics follow
+// Tiled row kernels (A <= kTileMaxA, the 10.yml / 100.yml shapes): one
+// 256-thread block per tile of 64 consecutive (b, v) rows, a quad of lanes per
+// row. The tile (64*A floats, contiguous in HBM) is copied into LDS by the
+// block with 16-B loads (fully coalesced, every byte read once), then each
+// quad runs its row out of LDS. Row statistics follow
 // Categorical(logits=masked) exactly as the group kernels: lse = m + log S
 // rounded in f32, l_j = x_j - lse, logprob = l_a, entropy = -sum q_j l_j
 // = lse - (sum p_j x_j)/S. Per-row results go to a row buffer; k_rowsum adds
 // them per sample in a fixed order (deterministic).
 constexpr int kTileMaxA = 128;
 
+// The whole block copies the tile once (thread t takes float4 t, t + 256, ...).
 __device__ __forceinline__ void tile_load(const float *src, float *lds, int n) {
-  const int lane = threadIdx.x & 63;
+  const int t = threadIdx.x, nt = blockDim.x;
   const int n4 = n >> 2;
   const float4 *s4 = reinterpret_cast<const float4 *>(src);
   float4 *d4 = reinterpret_cast<float4 *>(lds);
-  for (int i = lane; i < n4; i += 64) d4[i] = s4[i];
-  for (int i = (n4 << 2) + lane; i < n; i += 64) lds[i] = src[i];
+  for (int i = t; i < n4; i += nt) d4[i] = s4[i];
+  for (int i = (n4 << 2) + t; i < n; i += nt) lds[i] = src[i];
 }
 __device__ __forceinline__ void tile_store(float *dst, const float *lds, int n) {
-  const int lane = threadIdx.x & 63;
+  const int t = threadIdx.x, nt = blockDim.x;
   const int n4 = n >> 2;
   const float4 *s4 = reinterpret_cast<const float4 *>(lds);
   float4 *d4 = reinterpret_cast<float4 *>(dst);
-  for (int i = lane; i < n4; i += 64) d4[i] = s4[i];
-  for (int i = (n4 << 2) + lane; i < n; i += 64) dst[i] = lds[i];
+  for (int i = t; i < n4; i += nt) d4[i] = s4[i];
+  for (int i = (n4 << 2) + t; i < n; i += nt) dst[i] = lds[i];
 }
 
 // Quad layout inside a tile: wave w owns rows 16w..16w+15, lane l works on
