@@ -76,6 +76,17 @@ def ortho_init(layer, scale=np.sqrt(2)):
     return layer
 
 
+def _bf16_weight(w):
+    """bf16 copy of a parameter, made once per parameter version: AdamW's
+    in-place step bumps `_version`, so the copy is refreshed once per optimizer
+    step instead of at every forward of every update chunk."""
+    c = getattr(w, "_vmp_bf16", None)
+    if c is None or c[0] != w._version or c[1].shape != w.shape:
+        c = (w._version, w.detach().to(torch.bfloat16))
+        w._vmp_bf16 = c
+    return c[1]
+
+
 class BF16Linear(torch.autograd.Function):
     """y = x W^T + b with bf16 GEMM inputs and f32 accumulation / output
     (hipBLASLt through torch.mm(..., out_dtype=float32)); the backward GEMMs
@@ -85,7 +96,7 @@ class BF16Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b):
-        xb, wb = x.to(torch.bfloat16), w.to(torch.bfloat16)
+        xb, wb = x.to(torch.bfloat16), _bf16_weight(w)
         y = torch.mm(xb, wb.t(), out_dtype=torch.float32)
         if b is not None:
             y = y + b
