@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 4
+#define VMP_ABI_VERSION 5
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -77,6 +77,7 @@ extern "C" {
 #define VMP_HEAD_GIVEN 1  /* Network.get_action(obs, action, mask): log_prob/entropy only */
 #define VMP_HEAD_ARGMAX 2 /* Network.get_det_action (ppo.py:128-131): unmasked argmax */
 #define VMP_HEAD_MAX_A 1024 /* action_dim limit of the register-resident row */
+#define VMP_ACTOR_HEAD_MAX_A 256 /* action_dim limit of the fused GEMM + head (vmp_actor_head) */
 /* heuristic policies (src/agents/firstfit.py:21-38, bestfit.py:21-40) */
 #define VMP_POLICY_FIRSTFIT 0
 #define VMP_POLICY_BESTFIT 1
@@ -225,6 +226,22 @@ int vmp_policy_head_backward(int32_t B, int32_t V, int32_t A, const float *logit
                              const uint32_t *mask_bits, const int32_t *action,
                              const float *g_logprob, const float *g_entropy, float *dlogits,
                              void *hip_stream);
+
+/* The actor's last Linear fused with the head above (ppo.py:115-131, SURVEY
+ * §8(f)1): logits = h W^T + bias (h f32[B][K], weight f32[V*A][K] as nn.Linear
+ * stores it, bias f32[V*A]) computed on the f32 matrix cores and consumed by
+ * the head inside the same workgroup, so the [B, V*A] logits are never written
+ * unless logits_out (nullable, f32[B][V*A]) asks for them (the training
+ * forward keeps them for vmp_policy_head_backward). Modes, mask, coin flips,
+ * rng and outputs as vmp_policy_head, except that VMP_HEAD_SAMPLE draws by
+ * Gumbel-max (the same Categorical law; per-(call, row, column) counter
+ * uniforms). Needs K % 32 == 0, A <= VMP_ACTOR_HEAD_MAX_A and 16-byte aligned
+ * h / weight. */
+int vmp_actor_head(int32_t B, int32_t K, int32_t V, int32_t A, int32_t mode, const float *h,
+                   const float *weight, const float *bias, const uint32_t *mask_bits,
+                   float wait_ratio, int32_t wait_index, uint64_t seed, uint64_t offset,
+                   const uint64_t *rng_counter, int32_t *action, float *logprob, float *entropy,
+                   float *logits_out, float *workspace, void *hip_stream);
 
 /* Eval-mode Record metrics on the device (record.py:34-134, base.py:131-148):
  * on = 1 allocates the recorder and starts it from the current state (call it

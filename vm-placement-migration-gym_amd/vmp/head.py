@@ -153,6 +153,52 @@ def policy_head(logits, V, A, bits=None, action=None, rng: HeadRng = None, wait_
     return out
 
 
+ACTOR_HEAD_MAX_A = 256
+
+
+def actor_head_supported(h, weight, A):
+    """vmp_actor_head's shape contract (include/vmp.h)."""
+    return (h.is_cuda and h.dtype == torch.float32 and weight.dtype == torch.float32
+            and h.shape[-1] % 32 == 0 and A <= ACTOR_HEAD_MAX_A)
+
+
+def actor_head(h, weight, bias, V, A, bits=None, action=None, rng: HeadRng = None, mode=None,
+               wait_ratio=-1.0, wait_index=-1, logits_out=None):
+    """The actor's last Linear + the masked head in one launch (vmp_actor_head,
+    ppo.py:115-131): h f32 [B, K] -> (action i32 [B, V], logprob [B], entropy
+    [B]); the [B, V*A] logits are written only into `logits_out` if given.
+    mode: HEAD_SAMPLE (default without action), HEAD_GIVEN (default with
+    action) or HEAD_ARGMAX (get_det_action: action only). Not differentiable."""
+    _need_device(h, "actor_head")
+    h = h.contiguous()
+    B, K = h.shape
+    if mode is None:
+        mode = HEAD_SAMPLE if action is None else HEAD_GIVEN
+    if mode == HEAD_SAMPLE and rng is None:
+        raise ValueError("sampling needs a HeadRng")
+    if bits is not None and tuple(bits.shape) != (B, V, (A + 31) // 32):
+        raise ValueError(f"mask bits {tuple(bits.shape)} != {(B, V, (A + 31) // 32)}")
+    if mode == HEAD_GIVEN:
+        act = action.to(device=h.device, dtype=torch.int32).reshape(B, V).contiguous()
+    else:
+        act = torch.empty((B, V), dtype=torch.int32, device=h.device)
+    lp = ent = None
+    ws = None
+    if mode != HEAD_ARGMAX:
+        lp = torch.empty((B,), dtype=torch.float32, device=h.device)
+        ent = torch.empty((B,), dtype=torch.float32, device=h.device)
+        ws = torch.empty((2 * B * V,), dtype=torch.float32, device=h.device)
+    seed, off = rng.take(B * V) if (rng is not None and mode == HEAD_SAMPLE) else (0, 0)
+    ctr = rng.counter if rng is not None else None
+    check(lib().vmp_actor_head(B, K, V, A, mode, ptr(h), ptr(weight.contiguous()),
+                               ptr(bias.contiguous()), ptr(bits), float(wait_ratio),
+                               int(wait_index), seed, off, ptr(ctr), ptr(act), ptr(lp), ptr(ent),
+                               ptr(logits_out), ptr(ws), _stream(h)))
+    if rng is not None and mode == HEAD_SAMPLE:
+        rng.advance()
+    return act, lp, ent
+
+
 def det_action(logits, V, A):
     """get_det_action (ppo.py:128-131): unmasked argmax per VM row -> int32 [B, V]."""
     _need_device(logits, "det_action")
