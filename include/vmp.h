@@ -233,10 +233,9 @@ int vmp_policy_head_backward(int32_t B, int32_t V, int32_t A, const float *logit
  * the head inside the same workgroup, so the [B, V*A] logits are never written
  * unless logits_out (nullable, f32[B][V*A]) asks for them (the training
  * forward keeps them for vmp_policy_head_backward). Modes, mask, coin flips,
- * rng and outputs as vmp_policy_head, except that VMP_HEAD_SAMPLE draws by
- * Gumbel-max (the same Categorical law; per-(call, row, column) counter
- * uniforms). Needs K % 32 == 0, A <= VMP_ACTOR_HEAD_MAX_A and 16-byte aligned
- * h / weight. */
+ * rng and outputs as vmp_policy_head (the same per-row uniforms: equal logits
+ * draw equal actions). Needs K % 32 == 0, A <= VMP_ACTOR_HEAD_MAX_A and
+ * 16-byte aligned h / weight. */
 int vmp_actor_head(int32_t B, int32_t K, int32_t V, int32_t A, int32_t mode, const float *h,
                    const float *weight, const float *bias, const uint32_t *mask_bits,
                    float wait_ratio, int32_t wait_index, uint64_t seed, uint64_t offset,

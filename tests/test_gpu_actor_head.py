@@ -77,7 +77,7 @@ def test_argmax_matches_det_action():
 
 
 def test_sample_law_validity_and_stream():
-    """Gumbel-max draws follow softmax(masked logits) (5 sigma per category),
+    """Inverse-CDF draws follow softmax(masked logits) (5 sigma per category),
     never pick a masked action, and the stream advances between calls."""
     from vmp.head import HeadRng, actor_head, pack_mask
     V, A, K, B = 4, 12, 64, 40000
@@ -132,3 +132,20 @@ def test_wait_coin_flips_fused():
         assert abs((act[:, v] != P).double().mean().item() - expect) < 0.02, v
     assert (act[:, 6] == 5).all()
     assert abs((act[:, 7] != P).double().mean().item() - 0.7 * 11 / 12) < 0.02
+
+
+def test_sample_equals_unfused_draws():
+    """Fused and unfused heads take the same per-row uniform: on the same
+    weights they draw the same actions except where the f32 rounding of the
+    GEMM moves a CDF boundary across the uniform (rare)."""
+    from vmp.head import HeadRng, actor_head, pack_mask, policy_head
+    B, K, V, A = 2048, 512, 300, 102
+    h, w, b, mask, _ = _case(B, K, V, A, seed=11)
+    bits = pack_mask(mask, V, A)
+    with torch.no_grad():
+        a_f, lp_f, _ = actor_head(h, w, b, V, A, bits=bits, rng=HeadRng(5))
+        a_u, lp_u, _ = policy_head(torch.addmm(b, h, w.t()), V, A, bits=bits, rng=HeadRng(5))
+    same = (a_f == a_u).double().mean().item()
+    assert same > 0.999, same
+    rows = (a_f == a_u).all(1)
+    torch.testing.assert_close(lp_f[rows], lp_u[rows], rtol=1e-5, atol=1e-4 * V)

@@ -18,17 +18,18 @@
 // from LDS; the K order only changes f32 rounding, inside the 1e-5 contract).
 //
 // Epilogue: the C tile (+ bias) is staged in LDS, 64 rows at a time, and one
-// thread per (row, segment) applies the mask (`logits[mask] = -1e7`,
+// quad of lanes per (row, segment) applies the mask (`logits[mask] = -1e7`,
 // ppo.py:119) and the PPOAgent.act WAIT coin flip (ppo.py:154-156), then
 // lse = m + log S (f32, torch's Categorical order), logprob of the sampled /
-// given action, entropy -sum q (x - lse). SAMPLE draws by Gumbel-max over the
-// masked logits (counter-based uniforms per (call, row, column)): the same law
-// as Categorical.sample. ARGMAX is get_det_action: first max of the UNMASKED
-// row. Per-row results go to row_lp / row_ent; k_rowsum (vmp_policy.hip) adds
+// given action, entropy -sum q (x - lse). SAMPLE draws by inverse CDF with
+// one counter-based uniform per row (the unfused head's stream: equal logits
+// draw equal actions), the law of Categorical.sample. ARGMAX is
+// get_det_action: first max of the UNMASKED row. Per-row results go to row_lp / row_ent; k_rowsum (vmp_policy.hip) adds
 // them per sample in a fixed order.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/vmp.h"
 
@@ -39,7 +40,7 @@ __global__ void k_rowsum(int B, int V, const float *row_lp, const float *row_ent
 
 namespace {
 
-constexpr int kBM = 128, kBK = 32, kThreads = 512;
+constexpr int kBK = 32;
 constexpr int kLdsStride = kBK + 4;  // W tile row stride (floats)
 constexpr float kMasked = -1e7f;     // ppo.py:119
 
@@ -56,11 +57,6 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
 __device__ __forceinline__ float uniform_at(uint64_t seed, uint64_t ctr) {
   const uint64_t h = mix64(seed ^ mix64(ctr));
   return (float)(h >> 40) * (1.0f / 16777216.0f);
-}
-// open-interval uniform for the Gumbel noise (-log(-log u) stays finite)
-__device__ __forceinline__ float uniform_open(uint64_t seed, uint64_t ctr) {
-  const uint64_t h = mix64(seed ^ mix64(ctr));
-  return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
 }
 
 struct HGArgs {
@@ -79,11 +75,16 @@ __device__ __forceinline__ uint64_t eff_seed(const HGArgs &a) {
   return a.ctr ? a.seed ^ mix64(*a.ctr + 0x5851F42D4C957F2Dull) : a.seed;
 }
 
-template <int NT>
-__global__ __launch_bounds__(kThreads, 4) void k_head_gemm(HGArgs a) {
+// NW waves (BM = 16 NW rows) per workgroup, NT accumulator tiles per wave; 4
+// waves per SIMD (<= 128 VGPRs). Blocks are numbered M-fastest, so the
+// workgroups resident at a time share few W column slabs (L2 / MALL reuse).
+template <int NT, int NW>
+__global__ __launch_bounds__(64 * NW, 4) void k_head_gemm(HGArgs a) {
   extern __shared__ __align__(16) float lds[];
+  constexpr int kThreads = 64 * NW, kBM = 16 * NW;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int n_tile = blockIdx.x % a.n_tiles, m_blk = blockIdx.x / a.n_tiles;
+  const int m_blocks = (a.B + kBM - 1) / kBM;
+  const int m_blk = blockIdx.x % m_blocks, n_tile = blockIdx.x / m_blocks;
   const int m0 = m_blk * kBM;
   const int v0 = n_tile * a.S;                        // first VM row of the tile
   const int nseg = min(a.S, a.V - v0);                 // segments in this tile
@@ -162,6 +163,15 @@ __global__ __launch_bounds__(kThreads, 4) void k_head_gemm(HGArgs a) {
     __syncthreads();
   }
 
+#ifdef VMP_HG_GEMM_ONLY  // timing-only build: the main loop alone (outputs wrong)
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int c = 0; c < NT; c++) z += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+    if (z == 12345.f) a.row_lp[0] = z;  // keeps every MFMA live
+  }
+  return;
+#endif
   // ---- epilogue: 64 rows at a time through LDS (reuses the W buffers) ----
   const int BNp = a.BN + 1;  // odd row stride: the per-row scans hit distinct banks
   float *ct = lds;
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_head_gemm(HGArgs a) {
   const bool sample = a.mode == VMP_HEAD_SAMPLE, argmax = a.mode == VMP_HEAD_ARGMAX;
   const bool flip = a.wait_ratio >= 0.f && a.bits && !argmax;
 #pragma unroll 1
-  for (int half = 0; half < 2; half++) {
+  for (int half = 0; half < NW / 4; half++) {
     // waves 4*half .. 4*half+3 hold rows 64*half .. 64*half+63 of the tile
     if ((wid >> 2) == half) {
       const int rw = 16 * (wid & 3) + 4 * (lane >> 4);
@@ -192,20 +202,34 @@ __global__ __launch_bounds__(kThreads, 4) void k_head_gemm(HGArgs a) {
         a.logits[(int64_t)(m0 + 64 * half + r) * N + n0 + c] = ct[r * BNp + c];
       }
     }
-    for (int task = t; task < rows * nseg; task += kThreads) {
+    // one quad of lanes per (row, segment): lane c takes elements j = c + 4k
+    const int c = t & 3;
+#pragma unroll 1
+    for (int task = t >> 2; task < rows * nseg; task += kThreads >> 2) {
       const int r = task / nseg, s = task - r * nseg;
       const int b = m0 + 64 * half + r, v = v0 + s;
       const int64_t row = (int64_t)b * a.V + v;
       const float *x = ct + r * BNp + s * a.A;
       if (argmax) {  // get_det_action: first max of the unmasked row
-        float best = x[0];
-        int bi = 0;
-        for (int j = 1; j < a.A; j++)
-          if (x[j] > best || (best != best && x[j] == x[j])) {
-            best = x[j];
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int j = c; j < a.A; j += 4) {
+          const float xj = x[j];
+          if (xj == xj && (xj > best || bi == 0x7fffffff)) {
+            best = xj;
             bi = j;
           }
-        a.action[row] = bi;
+        }
+#pragma unroll
+        for (int o = 1; o < 4; o <<= 1) {
+          const float ob = __shfl_xor(best, o);
+          const int oi = __shfl_xor(bi, o);
+          if (ob > best || (ob == best && oi < bi)) {
+            best = ob;
+            bi = oi;
+          }
+        }
+        if (c == 0) a.action[row] = bi == 0x7fffffff ? 0 : bi;
         continue;
       }
       uint32_t mw[8];
@@ -228,52 +252,97 @@ __global__ __launch_bounds__(kThreads, 4) void k_head_gemm(HGArgs a) {
         return (((mw[j >> 5] >> (j & 31)) & 1u) || j == forbid) ? kMasked : x[j];
       };
       float m = -INFINITY;
-      for (int j = 0; j < a.A; j++) m = fmaxf(m, xm(j));
-      float S = 0.f, gbest = -INFINITY;
-      int gi = 0;
-      const uint64_t gctr = (a.offset + (uint64_t)row) << 10;
-      for (int j = 0; j < a.A; j++) {
-        const float xj = xm(j);
-        S += __expf(xj - m);
-        // Gumbel-max: masked entries take part only in an all-masked row (which
-        // torch samples uniformly); precise logs keep the noise finite for u
-        // near 1
-        if (sample && (xj != kMasked || m == kMasked)) {
-          const float key = xj - logf(-logf(uniform_open(seed, gctr | (uint64_t)j)));
-          if (key > gbest) {
-            gbest = key;
-            gi = j;
-          }
-        }
-      }
+      for (int j = c; j < a.A; j += 4) m = fmaxf(m, xm(j));
+      m = fmaxf(m, __shfl_xor(m, 1));
+      m = fmaxf(m, __shfl_xor(m, 2));
+      float sl = 0.f;  // this lane's share of S
+      for (int j = c; j < a.A; j += 4) sl += __expf(xm(j) - m);
+      float S = sl + __shfl_xor(sl, 1);
+      S += __shfl_xor(S, 2);
       const float lse = m + logf(S);
       // Categorical.entropy: -sum q_j (x_j - lse), the normalised logits rounded
       // in f32 as torch forms them (an all-masked row then gives lse's rounding)
       const float inv = 1.0f / S;
       float hs = 0.f;
-      for (int j = 0; j < a.A; j++) {
+      for (int j = c; j < a.A; j += 4) {
         const float xj = xm(j);
         const float p = __expf(xj - m);
         if (p > 0.f) hs += (p * inv) * (xj - lse);
       }
-      const int act = sample ? gi : a.action[row];
-      if (sample) a.action[row] = act;
-      a.row_lp[row] = (act >= 0 && act < a.A) ? xm(act) - lse : NAN;
-      a.row_ent[row] = -hs;
+      hs += __shfl_xor(hs, 1);
+      hs += __shfl_xor(hs, 2);
+      int act;
+      if (sample) {
+        // inverse CDF in lane-major order over the quad (vmp_policy.hip's tiled
+        // head: the same uniform per row, so equal logits draw equal actions)
+        float incl = sl + __shfl_up(sl, 1, 4) * (c >= 1);
+        incl += __shfl_up(incl, 2, 4) * (c >= 2);
+        const float excl = incl - sl;
+        const float total = __shfl(incl, 3, 4);
+        const float target = uniform_at(seed, a.offset + (uint64_t)row) * total;
+        int pick = -1, last = -1;
+        float cum = excl;
+        for (int j = c; j < a.A; j += 4) {
+          const float pj = __expf(xm(j) - m);
+          if (pj > 0.f) {
+            cum += pj;
+            last = j;
+            if (pick < 0 && target >= excl && target < cum) pick = j;
+          }
+        }
+        if (pick < 0 && last >= 0 && target >= excl && target < incl) pick = last;
+        int any = pick;
+#pragma unroll
+        for (int o = 1; o < 4; o <<= 1) any = max(any, __shfl_xor(any, o));
+        if (any < 0) {  // target past the rounded total: last positive entry
+          int lk = last >= 0 ? c * 1024 + last : -1;
+#pragma unroll
+          for (int o = 1; o < 4; o <<= 1) lk = max(lk, __shfl_xor(lk, o));
+          any = lk & 1023;
+        } else {  // more than one lane can claim only through rounding: lowest lane wins
+          int mine = pick >= 0 ? c : 4;
+#pragma unroll
+          for (int o = 1; o < 4; o <<= 1) mine = min(mine, __shfl_xor(mine, o));
+          any = __shfl(pick, mine, 4);
+        }
+        act = any;
+        if (c == 0) a.action[row] = act;
+      } else {
+        act = a.action[row];
+      }
+      if (c == 0) {
+        a.row_lp[row] = (act >= 0 && act < a.A) ? xm(act) - lse : NAN;
+        a.row_ent[row] = -hs;
+      }
     }
     __syncthreads();
   }
 }
 
-template <int NT>
-hipError_t launch_nt(const HGArgs &a, hipStream_t st) {
+template <int NT, int NW>
+hipError_t launch_nw(const HGArgs &a, hipStream_t st) {
   const size_t lds_w = (size_t)2 * NT * 16 * kLdsStride * sizeof(float);
   const size_t lds_c = (size_t)64 * (a.BN + 1) * sizeof(float);
   const size_t lds = lds_w > lds_c ? lds_w : lds_c;
-  const int64_t m_blocks = (a.B + kBM - 1) / kBM;
-  hipLaunchKernelGGL(k_head_gemm<NT>, dim3((unsigned)(m_blocks * a.n_tiles)), dim3(kThreads), lds,
-                     st, a);
+  const int64_t m_blocks = (a.B + 16 * NW - 1) / (16 * NW);
+  hipLaunchKernelGGL((k_head_gemm<NT, NW>), dim3((unsigned)(m_blocks * a.n_tiles)), dim3(64 * NW),
+                     lds, st, a);
   return hipGetLastError();
+}
+
+// 8 waves (128 rows per W slab) unless that leaves CUs idle; measured: 16
+// waves per workgroup (one per CU) ran 20 % slower, 4 waves 50 % slower at the
+// 100.yml shapes.
+template <int NT>
+hipError_t launch_nt(const HGArgs &a, hipStream_t st) {
+  const int64_t tiles = a.n_tiles;
+  if (const char *f = getenv("VMP_HG_NW")) {  // measurement override
+    if (f[0] == '4') return launch_nw<NT, 4>(a, st);
+    if (f[0] == '8') return launch_nw<NT, 8>(a, st);
+    if (f[0] == '1') return launch_nw<NT, 16>(a, st);
+  }
+  if (((a.B + 127) / 128) * tiles >= 256) return launch_nw<NT, 8>(a, st);
+  return launch_nw<NT, 4>(a, st);
 }
 
 }  // namespace
