@@ -77,7 +77,7 @@ extern "C" {
 #define VMP_HEAD_GIVEN 1  /* Network.get_action(obs, action, mask): log_prob/entropy only */
 #define VMP_HEAD_ARGMAX 2 /* Network.get_det_action (ppo.py:128-131): unmasked argmax */
 #define VMP_HEAD_MAX_A 1024 /* action_dim limit of the register-resident row */
-#define VMP_ACTOR_HEAD_MAX_A 256 /* action_dim limit of the fused GEMM + head (vmp_actor_head) */
+#define VMP_ACTOR_HEAD_MAX_A 128 /* action_dim limit of the fused GEMM + head (vmp_actor_head) */
 /* heuristic policies (src/agents/firstfit.py:21-38, bestfit.py:21-40) */
 #define VMP_POLICY_FIRSTFIT 0
 #define VMP_POLICY_BESTFIT 1

@@ -40,7 +40,7 @@ def _case(B, K, V, A, seed, p_mask=0.4):
 
 
 @pytest.mark.parametrize("B,K,V,A", [(64, 512, 30, 12), (200, 512, 300, 102), (37, 64, 7, 33),
-                                     (130, 96, 3, 250), (5, 32, 40, 208)])
+                                     (130, 96, 3, 128), (5, 32, 40, 120), (9, 64, 5, 65)])
 def test_given_mode_and_logits_match_unfused(B, K, V, A):
     from vmp.head import HEAD_GIVEN, actor_head, pack_mask, policy_head
     h, w, b, mask, act = _case(B, K, V, A, seed=B + K + V + A)
@@ -149,3 +149,34 @@ def test_sample_equals_unfused_draws():
     assert same > 0.999, same
     rows = (a_f == a_u).all(1)
     torch.testing.assert_close(lp_f[rows], lp_u[rows], rtol=1e-5, atol=1e-4 * V)
+
+
+def test_network_sample_fused_path_matches_logits_path():
+    """Network.sample / Network.det (the rollout paths of PPOTrainer.collect,
+    act_batch and ActStepGraph) on the fused kernel against the same network
+    through the logits path, at the config/100.yml action space."""
+    from vmp.head import HeadRng, actor_head_preferred, pack_mask
+    from vmp.ppo import Network
+    B, D, V, A = 512, 1100, 300, 102
+    assert actor_head_preferred(V, A)
+    torch.manual_seed(3)
+    net = Network(D, np.full(V, A), 64).to(DEV)
+    obs = torch.rand((B, D), device=DEV)
+    g = torch.Generator().manual_seed(4)
+    mask = torch.rand((B, V, A), generator=g) < 0.5
+    mask[..., A - 2] = False
+    bits = pack_mask(mask.to(DEV), V, A)
+    with torch.no_grad():
+        assert net._fused(obs)
+        net.rng = HeadRng(9)
+        a_f, lp_f = net.sample(obs, bits, wait_ratio=0.5, wait_index=A - 2)
+        d_f = net.det(obs)
+        net._fused = lambda o: False
+        net.rng = HeadRng(9)
+        a_u, lp_u = net.sample(obs, bits, wait_ratio=0.5, wait_index=A - 2)
+        d_u = net.det(obs)
+    assert (a_f == a_u).double().mean().item() > 0.999
+    assert not mask.to(DEV).gather(-1, a_f.long()[..., None]).any()
+    rows = (a_f == a_u).all(1)
+    torch.testing.assert_close(lp_f[rows], lp_u[rows], rtol=1e-5, atol=1e-4 * V)
+    assert (d_f == d_u).double().mean().item() > 0.999

@@ -153,13 +153,22 @@ def policy_head(logits, V, A, bits=None, action=None, rng: HeadRng = None, wait_
     return out
 
 
-ACTOR_HEAD_MAX_A = 256
+ACTOR_HEAD_MAX_A = 128
 
 
 def actor_head_supported(h, weight, A):
     """vmp_actor_head's shape contract (include/vmp.h)."""
     return (h.is_cuda and h.dtype == torch.float32 and weight.dtype == torch.float32
             and h.shape[-1] % 32 == 0 and A <= ACTOR_HEAD_MAX_A)
+
+
+def actor_head_preferred(V, A):
+    """Where the fused kernel beats logits GEMM + head (tools/bench_actor_head.py
+    on MI355X): wide action spaces. At config/100.yml (V*A = 30 600) the fused
+    rollout call is faster than hipBLASLt + the tiled head; at config/10.yml
+    (V*A = 360) the 360-column GEMM is too narrow to fill the chip and the
+    unfused path wins."""
+    return V * A >= 4096 and A <= ACTOR_HEAD_MAX_A
 
 
 def actor_head(h, weight, bias, V, A, bits=None, action=None, rng: HeadRng = None, mode=None,

@@ -168,6 +168,38 @@ class Network(nn.Module):
         return self._head(logits, self.V, self.A, bits=bits, action=action, rng=self.rng,
                           wait_ratio=wait_ratio, wait_index=wait_index)
 
+    def _fused(self, obs):
+        """The actor's last Linear + the HIP head as one kernel (vmp_actor_head)
+        where it is supported and faster; injected heads and bf16 GEMMs take the
+        logits path."""
+        last = self.actor[-1]
+        return (self._head is H.policy_head and self.precision == "f32" and obs.is_cuda
+                and obs.dtype == torch.float32 and H.actor_head_preferred(self.V, self.A)
+                and H.actor_head_supported(last.weight, last.weight, self.A))
+
+    def sample(self, obs, bits=None, wait_ratio=-1.0, wait_index=-1):
+        """Rollout sampling (ppo.py:115-126 with the mask as packed bits; the WAIT
+        coin flips of PPOAgent.act when wait_ratio >= 0) -> (action int32 [B, V],
+        logprob [B]). On the fused path the [B, V*A] logits never reach HBM."""
+        if self._fused(obs):
+            last = self.actor[-1]
+            h = self.actor[:-1](obs)
+            act, lp, _ = H.actor_head(h, last.weight, last.bias, self.V, self.A, bits=bits,
+                                      rng=self.rng, wait_ratio=wait_ratio, wait_index=wait_index)
+            return act, lp
+        act, lp, _ = self._head(self.actor_logits(obs), self.V, self.A, bits=bits, rng=self.rng,
+                                wait_ratio=wait_ratio, wait_index=wait_index)
+        return act, lp
+
+    def det(self, obs):
+        """get_det_action's argmax (ppo.py:128-131) -> int32 [B, V]."""
+        if self._fused(obs):
+            last = self.actor[-1]
+            act, _, _ = H.actor_head(self.actor[:-1](obs), last.weight, last.bias, self.V,
+                                     self.A, mode=H.HEAD_ARGMAX)
+            return act
+        return H.det_action(self.actor_logits(obs), self.V, self.A)
+
     def get_action(self, obs, action=None, invalid_mask=None):
         """ppo.py:115-126 -> (action int64 [B,V], logprob [B], entropy [B])."""
         logits = self.actor_logits(obs)
@@ -176,8 +208,7 @@ class Network(nn.Module):
 
     def get_det_action(self, obs, action=None):
         """ppo.py:128-131: argmax of the unmasked logits; [V] for one observation."""
-        logits = self.actor_logits(obs)
-        a = H.det_action(logits, self.V, self.A).long()
+        a = self.det(obs if obs.dim() > 1 else obs[None]).long()
         return a[0] if obs.dim() == 1 or obs.shape[0] == 1 else a
 
 
@@ -282,15 +313,12 @@ class PPOAgent(Base):
         """PPOAgent.act for every env of the batch on the device: int32 [N, V].
         The WAIT coin flips use the head's counter-based stream."""
         with torch.no_grad():
-            logits = self.model.actor_logits(obs)
             if self.config.det:
-                return H.det_action(logits, self.benv.V, self.benv.A)
+                return self.model.det(obs)
             if self.config.masked and bits is None:
                 bits = self.benv.mask_bits()
             ratio = float(self.config.migration_ratio) if self.config.masked else -1.0
-            act, _, _ = self.model._head(logits, self.benv.V, self.benv.A, bits=bits,
-                                         rng=self.model.rng, wait_ratio=ratio,
-                                         wait_index=self.benv.P)
+            act, _ = self.model.sample(obs, bits, wait_ratio=ratio, wait_index=self.benv.P)
             return act
 
     # ------------------------------------------------------------ weights
@@ -447,8 +475,7 @@ class PPOTrainer:
             bits = None
             if self.bits is not None:
                 bits = env.mask_bits(out=self.bits[t])
-            logits = m.actor_logits(o)
-            act, lp, _ = m._head(logits, self.V, self.A, bits=bits, rng=m.rng)
+            act, lp = m.sample(o, bits)
             self.act[t].copy_(act)
             self.logp[t].copy_(lp)
             nxt = self.obs[t + 1] if t + 1 < T else self.last_obs
