@@ -534,6 +534,7 @@ class PPOTrainer:
         eps = cfg.eps_clip
         params = [p for p in m.parameters()]
         stats = dict(minibatches=0, kl_breaks=0, clipfracs=[])
+        clipfracs = []  # device scalars, read once after the update (no per-minibatch sync)
         for epoch in range(cfg.k_epochs):
             for j in range(n_mb):
                 t0, t1 = j * mbs, min(T, (j + 1) * mbs)
@@ -547,8 +548,7 @@ class PPOTrainer:
                     std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
                     adv_n = (a_mb - mean) / (std + 1e-10)
                 ce = max(1, min(N, int(cfg.chunk_bytes) // max(1, mt * VA * 4)))
-                for p in params:
-                    p.grad = None
+                self._zero_grads(params)
                 kl_sum = torch.zeros(1, dtype=torch.float64, device=rew.device)
                 clip_n = torch.zeros(1, dtype=torch.float64, device=rew.device)
                 for n0 in range(0, N, ce):
@@ -590,33 +590,46 @@ class PPOTrainer:
                     loss.backward()
                     del logits
                 self._allreduce(kl_sum)
+                # the one host sync per minibatch: the reference's loop control
+                # (ppo.py:263-264) decides on the host whether this minibatch steps
                 kl = float(-kl_sum / m_glob)
                 if kl > cfg.kl_max:  # ppo.py:263-264: leaves this epoch's minibatch loop
-                    for p in params:
-                        p.grad = None
+                    self._zero_grads(params)
                     stats["kl_breaks"] += 1
                     break
                 self._allreduce(clip_n)
-                stats["clipfracs"].append(float(clip_n / m_glob))
-                if self.dist:
-                    self._allreduce_grads(params)
+                clipfracs.append(clip_n / m_glob)
+                if self.dist:  # the grads are views of one flat buffer: one all-reduce
+                    self.dist.all_reduce(self._gflat, group=self.group)
                 nn.utils.clip_grad_norm_(params, cfg.max_grad_norm)
                 self.agent.optimizer.step()
                 stats["minibatches"] += 1
                 stats["kl"] = kl
+        if clipfracs:
+            stats["clipfracs"] = torch.cat(clipfracs).double().cpu().tolist()
         self.stats = stats
         return stats
 
-    def _allreduce_grads(self, params):
-        """One RCCL all-reduce of the flat gradient."""
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        self.dist.all_reduce(flat, group=self.group)
-        o = 0
-        for p, g in zip(params, grads):
-            n = g.numel()
-            p.grad = flat[o:o + n].view_as(p)
-            o += n
+    def _zero_grads(self, params):
+        """Single process: grads re-created by backward. Data parallel: every
+        grad is a view of one flat f32 buffer, zeroed here, which backward
+        accumulates into and one RCCL all-reduce averages — no
+        per-step concatenation of the 69 MB of gradients."""
+        if not self.dist:
+            for p in params:
+                p.grad = None
+            return
+        n = sum(p.numel() for p in params)
+        if getattr(self, "_gflat", None) is None or self._gflat.numel() != n:
+            self._gflat = torch.zeros(n, dtype=params[0].dtype, device=params[0].device)
+            self._gviews = []
+            o = 0
+            for p in params:
+                self._gviews.append(self._gflat[o:o + p.numel()].view_as(p))
+                o += p.numel()
+        self._gflat.zero_()
+        for p, g in zip(params, self._gviews):
+            p.grad = g
 
     # ------------------------------------------------------------- driver
     def train_updates(self, n_updates):
