@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 5
+#define VMP_ABI_VERSION 6
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -226,6 +226,16 @@ int vmp_policy_head_backward(int32_t B, int32_t V, int32_t A, const float *logit
                              const uint32_t *mask_bits, const int32_t *action,
                              const float *g_logprob, const float *g_entropy, float *dlogits,
                              void *hip_stream);
+
+/* vmp_policy_head_backward with bf16 dlogits (round to nearest even), for the
+ * bf16-GEMM training leg whose dW / dh GEMMs take bf16 inputs: the cast pass
+ * over the [B, V*A] gradient is folded into the head's store. Tiled path only:
+ * A <= 128, logits 16-byte and dlogits 8-byte aligned; dlogits must not alias
+ * logits. Not a parity path (the reference trains in f32). */
+int vmp_policy_head_backward_bf16(int32_t B, int32_t V, int32_t A, const float *logits,
+                                  const uint32_t *mask_bits, const int32_t *action,
+                                  const float *g_logprob, const float *g_entropy,
+                                  uint16_t *dlogits_bf16, void *hip_stream);
 
 /* The actor's last Linear fused with the head above (ppo.py:115-131, SURVEY
  * §8(f)1): logits = h W^T + bias (h f32[B][K], weight f32[V*A][K] as nn.Linear

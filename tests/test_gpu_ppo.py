@@ -296,3 +296,40 @@ def test_bf16_training_runs_and_logprobs_are_consistent():
     assert st["kl_breaks"] == 0 and st["minibatches"] == 16
     assert any(not torch.equal(p0[k], v) for k, v in ag.model.state_dict().items())
     env.close()
+
+
+@pytest.mark.parametrize("V,A", [(30, 12), (300, 102)])
+def test_bf16_actor_head_node_equals_linear_plus_head(V, A):
+    """BF16ActorHead (the bf16 leg's last Linear + head as one node, bf16 dlogits
+    from vmp_policy_head_backward_bf16) against BF16Linear followed by the HIP
+    head: logprob / entropy and dh, dW equal (the same bf16 rounding of the same
+    f32 dlogits); the bias gradient sums bf16-rounded dlogits, so it agrees to
+    bf16 rounding of the f32 sum."""
+    from vmp.head import pack_mask, policy_head
+    from vmp.ppo import BF16ActorHead, BF16Linear
+    g = torch.Generator().manual_seed(V + A)
+    B, K = 96, 64
+    x = torch.randn(B, K, generator=g).to(DEV)
+    w = (torch.randn(V * A, K, generator=g) * 0.1).to(DEV)
+    b = (torch.randn(V * A, generator=g) * 0.1).to(DEV)
+    mask = torch.rand((B, V, A), generator=g) < 0.4
+    mask[..., A - 2] = False
+    mask[0, 0] = True  # an all-masked row
+    bits = pack_mask(mask.to(DEV), V, A)
+    act = torch.randint(0, A - 2, (B, V), generator=g).to(DEV)
+    glp, gen = torch.randn(B, generator=g).to(DEV), torch.randn(B, generator=g).to(DEV)
+    outs = []
+    for fused in (True, False):
+        xi, wi, bi = (t.clone().requires_grad_(True) for t in (x, w, b))
+        if fused:
+            lp, ent = BF16ActorHead.apply(xi, wi, bi, bits, act, V, A)
+        else:
+            _, lp, ent = policy_head(BF16Linear.apply(xi, wi, bi), V, A, bits=bits, action=act)
+        (lp * glp + ent * gen).sum().backward()
+        outs.append((lp.detach(), ent.detach(), xi.grad, wi.grad, bi.grad))
+    (lp1, e1, gx1, gw1, gb1), (lp2, e2, gx2, gw2, gb2) = outs
+    torch.testing.assert_close(lp1, lp2, rtol=1e-5, atol=1e-5 * V)
+    torch.testing.assert_close(e1, e2, rtol=1e-5, atol=1e-5 * V)
+    torch.testing.assert_close(gx1, gx2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gw1, gw2, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(gb1, gb2, rtol=1e-2, atol=1e-2 * gb2.abs().max().item())

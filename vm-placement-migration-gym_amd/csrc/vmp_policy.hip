@@ -66,6 +66,7 @@ struct HeadArgs {
   float *entropy;        // [B] (nullable)
   const float *g_logprob, *g_entropy;  // backward: dL/dlogprob[B], dL/dentropy[B]
   float *dlogits;        // backward output [B][V][A] (may alias logits)
+  uint16_t *dlogits_bf16;  // or: bf16 backward output [B][V][A] (tiles only)
   float *row_lp, *row_ent;  // tiled kernels: per-row results [B*V]
 };
 
@@ -323,6 +324,24 @@ __device__ __forceinline__ void tile_store(float *dst, const float *lds, int n) 
   for (int i = (n4 << 2) + t; i < n; i += nt) dst[i] = lds[i];
 }
 
+// f32 tile -> bf16 rows (round to nearest even, v_cvt_pk_bf16_f32), 8-B stores
+__device__ __forceinline__ void tile_store_bf16(uint16_t *dst, const float *lds, int n) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int n4 = n >> 2;
+  const float4 *s4 = reinterpret_cast<const float4 *>(lds);
+  for (int i = t; i < n4; i += nt) {
+    const float4 v = s4[i];
+    const __bf16 h[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    uint2 u;
+    __builtin_memcpy(&u, h, 8);
+    reinterpret_cast<uint2 *>(dst)[i] = u;
+  }
+  for (int i = (n4 << 2) + t; i < n; i += nt) {
+    const __bf16 h = (__bf16)lds[i];
+    __builtin_memcpy(dst + i, &h, 2);
+  }
+}
+
 // Quad layout inside a tile: wave w owns rows 16w..16w+15, lane l works on
 // row 16w + l/4 with the 4 lanes of its quad taking elements j = c + 4k
 // (c = l%4): row reductions are 2 quad shuffles (DPP), per-lane work is A/4.
@@ -527,7 +546,8 @@ __global__ __launch_bounds__(256) void k_head_bwd_tile(HeadArgs a) {
     }
   }
   __syncthreads();
-  tile_store(a.dlogits + r0 * a.A, tl, nr * a.A);
+  if (a.dlogits_bf16) tile_store_bf16(a.dlogits_bf16 + r0 * a.A, tl, nr * a.A);
+  else tile_store(a.dlogits + r0 * a.A, tl, nr * a.A);
 }
 
 // Per-sample sums of the row results (ppo.py:124-125), fixed order: one wave per sample.
@@ -695,6 +715,26 @@ int vmp_policy_head_backward(int32_t B, int32_t V, int32_t A, const float *logit
   a.wait_ratio = -1.f;
   a.logits = logits, a.bits = mask_bits, a.action = const_cast<int32_t *>(action);
   a.g_logprob = g_logprob, a.g_entropy = g_entropy, a.dlogits = dlogits;
+  hipError_t e = launch_bwd(a, (hipStream_t)stream);
+  if (e != hipSuccess) return vmp::policy_fail(VMP_EDEVICE, hipGetErrorString(e));
+  return VMP_OK;
+}
+
+int vmp_policy_head_backward_bf16(int32_t B, int32_t V, int32_t A, const float *logits,
+                                  const uint32_t *mask_bits, const int32_t *action,
+                                  const float *g_logprob, const float *g_entropy,
+                                  uint16_t *dlogits_bf16, void *stream) {
+  if (B < 0 || V < 1 || A < 1 || A > VMP_HEAD_MAX_A || !logits || !action || !dlogits_bf16)
+    return vmp::policy_fail(VMP_EINVAL, "vmp_policy_head_backward_bf16: bad shape or null pointer");
+  if (B == 0) return VMP_OK;
+  HeadArgs a{};
+  a.B = B, a.V = V, a.A = A, a.W = (A + 31) / 32, a.mode = VMP_HEAD_GIVEN, a.wait_index = -1;
+  a.wait_ratio = -1.f;
+  a.logits = logits, a.bits = mask_bits, a.action = const_cast<int32_t *>(action);
+  a.g_logprob = g_logprob, a.g_entropy = g_entropy, a.dlogits_bf16 = dlogits_bf16;
+  if (!use_tiles(a) || ((uintptr_t)dlogits_bf16 & 7))
+    return vmp::policy_fail(VMP_EINVAL, "vmp_policy_head_backward_bf16: needs A <= 128, 16-B aligned "
+                                        "logits and 8-B aligned dlogits");
   hipError_t e = launch_bwd(a, (hipStream_t)stream);
   if (e != hipSuccess) return vmp::policy_fail(VMP_EDEVICE, hipGetErrorString(e));
   return VMP_OK;

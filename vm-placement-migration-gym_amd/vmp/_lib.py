@@ -16,7 +16,8 @@ EXPORTS = (
     "vmp_set_eval", "vmp_dims", "vmp_reset", "vmp_step", "vmp_heuristic_act",
     "vmp_heuristic_step", "vmp_rollout_heuristic", "vmp_mask", "vmp_mask_bool", "vmp_get_obs",
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
-    "vmp_policy_head", "vmp_policy_head_backward", "vmp_actor_head", "vmp_record_enable",
+    "vmp_policy_head", "vmp_policy_head_backward", "vmp_policy_head_backward_bf16",
+    "vmp_actor_head", "vmp_record_enable",
     "vmp_record_read",
     "vmp_debug_stamps",
 )
@@ -87,6 +88,7 @@ def lib():
         "vmp_policy_head": (ctypes.c_int, [i32, i32, i32, i32, P, P, f32, i32, u64, u64, P, P, P,
                                             P, P, P]),
         "vmp_policy_head_backward": (ctypes.c_int, [i32, i32, i32, P, P, P, P, P, P, P]),
+        "vmp_policy_head_backward_bf16": (ctypes.c_int, [i32, i32, i32, P, P, P, P, P, P, P]),
         "vmp_actor_head": (ctypes.c_int, [i32, i32, i32, i32, i32, P, P, P, P, f32, i32, u64, u64,
                                            P, P, P, P, P, P, P]),
         "vmp_record_enable": (ctypes.c_int, [P, i32]),
@@ -96,7 +98,7 @@ def lib():
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 5:
+    if L.vmp_abi_version() != 6:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

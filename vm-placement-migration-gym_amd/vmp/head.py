@@ -136,6 +136,34 @@ class MaskedHead(torch.autograd.Function):
         return d, None, None, None, None, None, None, None, None, None
 
 
+HEAD_TILE_MAX_A = 128  # kTileMaxA: the tiled kernels (and the bf16 backward)
+
+
+def head_given(logits, V, A, bits, action):
+    """vmp_policy_head in GIVEN mode outside autograd -> (logprob [B], entropy [B])."""
+    _need_device(logits, "head_given")
+    B = logits.shape[0]
+    act = action.to(device=logits.device, dtype=torch.int32).reshape(B, V).contiguous()
+    lp = torch.empty((B,), dtype=torch.float32, device=logits.device)
+    ent = torch.empty((B,), dtype=torch.float32, device=logits.device)
+    ws = torch.empty((2 * B * V,), dtype=torch.float32, device=logits.device)
+    check(lib().vmp_policy_head(B, V, A, HEAD_GIVEN, ptr(logits), ptr(bits), -1.0, -1, 0, 0, None,
+                                ptr(act), ptr(lp), ptr(ent), ptr(ws), _stream(logits)))
+    return act, lp, ent
+
+
+def head_backward_bf16(logits, V, A, bits, act, g_lp, g_ent):
+    """vmp_policy_head_backward_bf16: the head's dlogits rounded to bf16 in its
+    store -> bf16 [B, V*A] (the bf16 training leg's GEMM input)."""
+    B = logits.shape[0]
+    d = torch.empty((B, V * A), dtype=torch.bfloat16, device=logits.device)
+    glp = None if g_lp is None else g_lp.float().contiguous()
+    gen = None if g_ent is None else g_ent.float().contiguous()
+    check(lib().vmp_policy_head_backward_bf16(B, V, A, ptr(logits), ptr(bits), ptr(act), ptr(glp),
+                                              ptr(gen), ptr(d), _stream(logits)))
+    return d
+
+
 def policy_head(logits, V, A, bits=None, action=None, rng: HeadRng = None, wait_ratio=-1.0,
                 wait_index=-1):
     """Functional form of MaskedHead (differentiable in logits)."""

@@ -87,6 +87,24 @@ def _bf16_weight(w):
     return c[1]
 
 
+_ADDMM_OUT_DTYPE = None
+
+
+def _addmm_f32(b, xb, wb):
+    """b + xb wb^T with bf16 inputs and f32 accumulate / output, the bias added
+    in the GEMM's epilogue (torch.addmm(..., out_dtype=float32)) where this
+    torch build has it, else as a separate add."""
+    global _ADDMM_OUT_DTYPE
+    if _ADDMM_OUT_DTYPE is not False:
+        try:
+            y = torch.addmm(b, xb, wb.t(), out_dtype=torch.float32)
+            _ADDMM_OUT_DTYPE = True
+            return y
+        except (TypeError, RuntimeError, NotImplementedError):
+            _ADDMM_OUT_DTYPE = False
+    return torch.mm(xb, wb.t(), out_dtype=torch.float32) + b
+
+
 class BF16Linear(torch.autograd.Function):
     """y = x W^T + b with bf16 GEMM inputs and f32 accumulation / output
     (hipBLASLt through torch.mm(..., out_dtype=float32)); the backward GEMMs
@@ -97,9 +115,10 @@ class BF16Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         xb, wb = x.to(torch.bfloat16), _bf16_weight(w)
-        y = torch.mm(xb, wb.t(), out_dtype=torch.float32)
         if b is not None:
-            y = y + b
+            y = _addmm_f32(b, xb, wb)
+        else:
+            y = torch.mm(xb, wb.t(), out_dtype=torch.float32)
         ctx.save_for_backward(xb, wb)
         ctx.has_bias = b is not None
         return y
@@ -112,6 +131,35 @@ class BF16Linear(torch.autograd.Function):
         gw = torch.mm(g.t(), xb, out_dtype=torch.float32) if ctx.needs_input_grad[1] else None
         gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
+
+
+class BF16ActorHead(torch.autograd.Function):
+    """The bf16 leg's last actor Linear and the masked head (GIVEN actions) as one
+    autograd node -> (logprob [B], entropy [B]). Forward: bias in the GEMM
+    epilogue, f32 logits to the HIP head. Backward: the head writes dlogits in
+    bf16 (vmp_policy_head_backward_bf16), which feed the dW / dh GEMMs as they
+    are; the bias gradient sums them with f32 accumulation. Saves the passes an
+    nn.Linear + head graph makes over the [B, V*A] logits: the bias add, the
+    f32 -> bf16 cast of dlogits and the f32 bias-gradient read."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, bits, action, V, A):
+        xb, wb = x.to(torch.bfloat16), _bf16_weight(w)
+        logits = _addmm_f32(b, xb, wb)
+        act, lp, ent = H.head_given(logits, V, A, bits, action)
+        ctx.save_for_backward(logits, bits, act, xb, wb)
+        ctx.V, ctx.A = V, A
+        return lp, ent
+
+    @staticmethod
+    def backward(ctx, g_lp, g_ent):
+        logits, bits, act, xb, wb = ctx.saved_tensors
+        g = H.head_backward_bf16(logits, ctx.V, ctx.A, bits, act, g_lp, g_ent)
+        del logits
+        gx = torch.mm(g, wb, out_dtype=torch.float32) if ctx.needs_input_grad[0] else None
+        gw = torch.mm(g.t(), xb, out_dtype=torch.float32) if ctx.needs_input_grad[1] else None
+        gb = g.sum(0, dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        return gx, gw, gb, None, None, None, None
 
 
 def _run_mlp(seq, x, precision):
@@ -199,6 +247,19 @@ class Network(nn.Module):
                                      self.A, mode=H.HEAD_ARGMAX)
             return act
         return H.det_action(self.actor_logits(obs), self.V, self.A)
+
+    def logprob_entropy(self, obs, bits, action):
+        """get_action(obs, action, mask)'s logprob and entropy (ppo.py:115-126) for
+        the update, differentiable. The bf16 leg with the HIP head runs the last
+        Linear and the head as one node (BF16ActorHead)."""
+        if (self.precision == "bf16" and self._head is H.policy_head and obs.is_cuda
+                and self.A <= H.HEAD_TILE_MAX_A):
+            last = self.actor[-1]
+            h = _run_mlp(self.actor[:-1], obs, "bf16")
+            return BF16ActorHead.apply(h, last.weight, last.bias, bits, action, self.V, self.A)
+        _, lp, ent = self._head(self.actor_logits(obs), self.V, self.A, bits=bits, action=action,
+                                rng=self.rng)
+        return lp, ent
 
     def get_action(self, obs, action=None, invalid_mask=None):
         """ppo.py:115-126 -> (action int64 [B,V], logprob [B], entropy [B])."""
@@ -557,9 +618,7 @@ class PPOTrainer:
                     o = obs[t0:t1, n0:n1].reshape(mt * nc, -1)
                     b = None if bits is None else bits[t0:t1, n0:n1].reshape(mt * nc, self.V, -1)
                     a = act[t0:t1, n0:n1].reshape(mt * nc, self.V)
-                    logits = m.actor_logits(o)
-                    _, newlp, ent = m._head(logits, self.V, self.A, bits=b, action=a,
-                                            rng=m.rng)
+                    newlp, ent = m.logprob_entropy(o, b, a)
                     newlp = newlp.reshape(mt, nc)
                     logratio = newlp - old_lp[t0:t1, n0:n1]
                     ratio = torch.exp(logratio)
@@ -588,7 +647,6 @@ class PPOTrainer:
                         lvf = (du * du).sum() / denom
                     loss = loss_clip - cfg.ent_coef * ent.sum() / m_glob + cfg.vf_coef * 0.5 * lvf
                     loss.backward()
-                    del logits
                 self._allreduce(kl_sum)
                 # the one host sync per minibatch: the reference's loop control
                 # (ppo.py:263-264) decides on the host whether this minibatch steps
