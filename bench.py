@@ -376,7 +376,7 @@ def bench_stress(args, dev, rank, world, dist):
             "mean_waiting": waiting, "ms_per_step": 1e3 * el / K, "kernel_ms": kern_ms,
             "bytes_per_env_step": bpe,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "kernel": "vmp::k_env_big<20>"}}
+                         "frac": ach / HBM_PEAK_GBS, "kernel": "vmp::k_env_big<20, true>"}}
 
 
 def bench_external(args, env, dev, stream, dist, world, P, V):

@@ -18,9 +18,8 @@ namespace vmp {
 constexpr int kStamps = 24;  // per-env phase clocks (diagnostic builds)
 template <int VPT, bool ONE>
 __global__ void k_env(EnvParams p, StepOut o);
-template <int SPT>
+template <int SPT, bool ONE>
 __global__ void k_env_big(EnvParams p, StepOut o);
-extern template __global__ void k_env_big<20>(EnvParams p, StepOut o);
 __global__ void k_rank(EnvParams p, int64_t *rank);
 __global__ void k_target_means_lds(EnvParams p);
 constexpr int kBigMaxThreads = 512;  // k_env_big: one workgroup per env
@@ -214,6 +213,15 @@ void launch_vpt(int need, dim3 grid, dim3 block, size_t lds, hipStream_t s, cons
   else hipLaunchKernelGGL((k_env<16, ONE>), grid, block, lds, s, p, o);
 }
 
+template <bool ONE>
+void launch_big(int spt, dim3 grid, dim3 block, size_t lds, hipStream_t s, const EnvParams &p,
+                const StepOut &o) {
+  if (spt == 4) hipLaunchKernelGGL((k_env_big<4, ONE>), grid, block, lds, s, p, o);
+  else if (spt == 8) hipLaunchKernelGGL((k_env_big<8, ONE>), grid, block, lds, s, p, o);
+  else if (spt == 16) hipLaunchKernelGGL((k_env_big<16, ONE>), grid, block, lds, s, p, o);
+  else hipLaunchKernelGGL((k_env_big<20, ONE>), grid, block, lds, s, p, o);
+}
+
 // k_env_big's shape: the fewest slots per thread that fit 512 threads, and the
 // thread count (whole waves). The block's VM words live in LDS (4 B per slot).
 void big_shape(int64_t V, int &spt, int &nt) {
@@ -235,10 +243,8 @@ int launch_env(vmp_handle *h, const StepOut &o) {
     int spt, nt;
     big_shape(h->V, spt, nt);
     const size_t lds1 = (size_t)p.lds_wave_bytes + 4 * (size_t)spt * nt;
-    if (spt == 4) hipLaunchKernelGGL(k_env_big<4>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
-    else if (spt == 8) hipLaunchKernelGGL(k_env_big<8>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
-    else if (spt == 16) hipLaunchKernelGGL(k_env_big<16>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
-    else hipLaunchKernelGGL(k_env_big<20>, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
+    if (o.k_steps == 1) launch_big<true>(spt, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
+    else launch_big<false>(spt, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
     HIP_TRY(hipGetLastError());
     return VMP_OK;
   }

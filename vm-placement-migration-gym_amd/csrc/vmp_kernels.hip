@@ -217,24 +217,31 @@ __device__ __forceinline__ int64_t poisson(Pcg &r, const PoisConst &c) {
 // accumulated per env into p.stamps[e][kStamps]. No stamp executes otherwise.
 #ifdef VMP_STAMPS
 constexpr int kStamps = 24;
-#define STAMP_PARAMS , uint64_t (&st_acc)[kStamps], uint64_t &st_prev
+// The accumulators live in LDS (one row per wave in k_env, one per block in
+// k_env_big, written by one lane), not in registers: a 24-entry register
+// array in the 256-VGPR block kernel spilled and distorted its timing ~7x.
+#define STAMP_PARAMS , uint64_t LDSP *st_acc, uint64_t &st_prev
 #define STAMP_ARGS , st_acc, st_prev
-#define STAMP_DECL uint64_t st_acc[kStamps] = {0}, st_prev = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                   \
-  do {                                             \
+#define STAMP_DECL_AT(ptr)                                          \
+  uint64_t LDSP *st_acc = (ptr);                                    \
+  if (st_acc && lane_id() == 0)                                     \
+    for (int _i = 0; _i < kStamps; _i++) st_acc[_i] = 0;            \
+  uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                      \
+  do {                                                \
     const uint64_t _t = __builtin_amdgcn_s_memtime(); \
-    st_acc[i] += _t - st_prev;                     \
-    st_prev = _t;                                  \
+    if (st_acc && lane_id() == 0) st_acc[i] += _t - st_prev; \
+    st_prev = _t;                                     \
   } while (0)
 #define STAMP_FLUSH()                                                         \
   do {                                                                        \
-    if (p.stamps && lane == 0)                                                \
+    if (p.stamps && st_acc && lane_id() == 0)                                 \
       for (int _i = 0; _i < kStamps; _i++) p.stamps[(int64_t)e * kStamps + _i] += st_acc[_i]; \
   } while (0)
 #else
 #define STAMP_PARAMS
 #define STAMP_ARGS
-#define STAMP_DECL
+#define STAMP_DECL_AT(ptr)
 #define STAMP(i)
 #define STAMP_FLUSH()
 #endif
@@ -1736,11 +1743,16 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
     if (j * 64 + lane < n_pm) L.cpu[j * 64 + lane] = pv[j];
   for (int i = 256 + lane; i < n_pm; i += 64) L.cpu[i] = pm[i];  // P > 128
   wsync();
-  STAMP_DECL
 #ifdef VMP_STAMPS
-  st_acc[13] = t_loaded - t_start;
-  st_acc[14] = t_drawn - t_loaded;
-  st_acc[15] = st_prev - t_drawn;
+  __shared__ uint64_t st_lds[kEnvWavesPerBlock * kStamps];
+#endif
+  STAMP_DECL_AT((uint64_t LDSP *)st_lds + wid * kStamps)
+#ifdef VMP_STAMPS
+  if (lane == 0) {
+    st_acc[13] = t_loaded - t_start;
+    st_acc[14] = t_drawn - t_loaded;
+    st_acc[15] = st_prev - t_drawn;
+  }
 #endif
   bool term = false;
   int64_t ndone = 0;
@@ -1794,8 +1806,10 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
   }
   STAMP(6);
 #ifdef VMP_STAMPS
-  st_acc[7] = (__builtin_amdgcn_s_memrealtime() - rt_start) * 1000;  // x1000 (100 MHz ticks)
-  st_acc[9] = __builtin_amdgcn_s_memtime() - t_start;
+  if (lane == 0) {
+    st_acc[7] = (__builtin_amdgcn_s_memrealtime() - rt_start) * 1000;  // x1000 (100 MHz ticks)
+    st_acc[9] = __builtin_amdgcn_s_memtime() - t_start;
+  }
 #endif
   STAMP_FLUSH();
 }
@@ -1984,6 +1998,11 @@ __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, ui
 #endif
 
 constexpr int kBigMaxSPT = 20, kBigMaxWaves = 8;
+// k_env_big's per-step helpers (pairwise-sum jobs, reward, draws): out of line
+// by default; -DVMP_BIG_CALL=__forceinline__ inlines them (A/B build)
+#ifndef VMP_BIG_CALL
+#define VMP_BIG_CALL __noinline__
+#endif
 struct BigShared {
   int32_t wcnt[16];   // per-wave counts of a compaction
   int32_t bc[8];      // broadcast scalars
@@ -2319,7 +2338,7 @@ VMP_SLOOP
 // numpy's pairwise order. Out of line so its temporaries do not share the
 // register budget with the block's slot arrays.
 constexpr int kBigPwDepth = 6;  // register plan up to n = 7688
-__device__ __noinline__ void big_sum_job(const EnvParams &p, const Tables &T, char LDSP *base,
+__device__ VMP_BIG_CALL void big_sum_job(const EnvParams &p, const Tables &T, char LDSP *base,
                                          int j, int k, int n_ex) {
   const Lds L = make_lds(p, base);
   const int P = p.P;
@@ -2370,7 +2389,7 @@ __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &
 }
 
 // Wave 0 of k_env_big after the sums: reward, counters and termination.
-__device__ __noinline__ void big_stats_final(const EnvParams &p, BigShared &B, char LDSP *base,
+__device__ VMP_BIG_CALL void big_stats_final(const EnvParams &p, BigShared &B, char LDSP *base,
                                              int64_t k, int n_ex, int n_w, int64_t n_term,
                                              int64_t arrivals) {
   const Lds L = make_lds(p, base);
@@ -2427,7 +2446,7 @@ __device__ __noinline__ void big_stats_final(const EnvParams &p, BigShared &B, c
   wsync();
 }
 
-__device__ __noinline__ void big_predraw(const EnvParams &p, const Tables &T, char LDSP *base,
+__device__ VMP_BIG_CALL void big_predraw(const EnvParams &p, const Tables &T, char LDSP *base,
                                          int K, const uint64_t *jt) {
   const Lds L = make_lds(p, base);
   const U128 JA{jt[0], jt[1]}, JM{jt[2], jt[3]};
@@ -2641,7 +2660,10 @@ VMP_SLOOP
   return reward;
 }
 
-template <int SPT>
+// ONE = true: the per-step launch (k_steps == 1), its own instantiation so the
+// step's registers (rem[] above all) are dead after the state store instead of
+// live around the K-step loop's back edge, which spilled them around the sums.
+template <int SPT, bool ONE>
 __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   extern __shared__ __align__(16) char lds[];
   __shared__ Tables T;
@@ -2652,7 +2674,10 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   const Lds L = make_lds(p, (char LDSP *)lds);
   uint32_t LDSP *W = reinterpret_cast<uint32_t LDSP *>((char LDSP *)lds + p.lds_wave_bytes);
   const int V = p.V, P = p.P;
-  STAMP_DECL
+#ifdef VMP_STAMPS
+  __shared__ uint64_t st_lds[kStamps];
+#endif
+  STAMP_DECL_AT(w0 ? (uint64_t LDSP *)st_lds : nullptr)  // thread 0's clock
   for (int i = t; i < 128; i += NT) {
     T.cent[i] = (double)i / 100.0;
     T.fcent[i] = (float)((double)i / 100.0);
@@ -2697,9 +2722,10 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   STAMP(13);
   bool term = false;
   int64_t ndone = 0;
+  const int k_steps = ONE ? 1 : o.k_steps;
 #pragma unroll 1
-  for (int k = 0; k < o.k_steps; k++) {
-    const bool last = k == o.k_steps - 1;
+  for (int k = 0; k < k_steps; k++) {
+    const bool last = k == k_steps - 1;
     uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
     int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
     int64_t n_place = 0, n_susp = 0;
@@ -2767,16 +2793,17 @@ VMP_SLOOP
     if (t < 32)
       reinterpret_cast<uint64_t *>(p.hdr + e)[t] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
   }
-#ifdef VMP_STAMPS
   STAMP(6);
-  if (p.stamps && t == 0)
-    for (int _i = 0; _i < kStamps; _i++) p.stamps[(int64_t)e * kStamps + _i] += st_acc[_i];
-#endif
+  STAMP_FLUSH();
 }
-template __global__ void k_env_big<4>(EnvParams, StepOut);
-template __global__ void k_env_big<8>(EnvParams, StepOut);
-template __global__ void k_env_big<16>(EnvParams, StepOut);
-template __global__ void k_env_big<20>(EnvParams, StepOut);
+template __global__ void k_env_big<4, false>(EnvParams, StepOut);
+template __global__ void k_env_big<8, false>(EnvParams, StepOut);
+template __global__ void k_env_big<16, false>(EnvParams, StepOut);
+template __global__ void k_env_big<20, false>(EnvParams, StepOut);
+template __global__ void k_env_big<4, true>(EnvParams, StepOut);
+template __global__ void k_env_big<8, true>(EnvParams, StepOut);
+template __global__ void k_env_big<16, true>(EnvParams, StepOut);
+template __global__ void k_env_big<20, true>(EnvParams, StepOut);
 
 // _get_rank for any V: one wave per env, LDS bitmap of used PMs.
 __global__ __launch_bounds__(64) void k_rank(EnvParams p, int64_t *rank) {
