@@ -2012,6 +2012,7 @@ struct BigShared {
   uint32_t evw[512];  // event list (one slot row of the block): VM word
   int32_t evt[512];   // event list: target / value
   uint8_t evok[512];  // event results
+  double half[20];    // big_sum_phase: the two halves of a split job j at 2j, 2j + 1
 };
 
 // Rank of this thread's flag among the flagged threads of the block
@@ -2338,54 +2339,79 @@ VMP_SLOOP
 // numpy's pairwise order. Out of line so its temporaries do not share the
 // register budget with the block's slot arrays.
 constexpr int kBigPwDepth = 6;  // register plan up to n = 7688
+// Job j over elements [o, o + m) of its source (the whole job: o = 0, m = n),
+// result to *dst.
 __device__ VMP_BIG_CALL void big_sum_job(const EnvParams &p, const Tables &T, char LDSP *base,
-                                         int j, int k, int n_ex) {
+                                         int j, int n_ex, int o, int m, double LDSP *dst) {
   const Lds L = make_lds(p, base);
   const int P = p.P;
   double LDSP *res = L.jobres;
   const double *cent = T.cent;
   double r;
   if (j < 4) {
-    const uint8_t LDSP *src = (j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp);
-    r = wave_pw_sum<kBigPwDepth>(j < 2 ? k : n_ex, [=](int i) { return cent[src[i]]; }, L.pw);
+    const uint8_t LDSP *src = ((j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp)) + o;
+    r = wave_pw_sum<kBigPwDepth>(m, [=](int i) { return cent[src[i]]; }, L.pw);
   } else if (j < 8) {
-    const double LDSP *src = (j & 1) ? L.mem : L.cpu;
+    const double LDSP *src = ((j & 1) ? L.mem : L.cpu) + o;
     const double mean = j < 6 ? 0.0 : res[j - 2] / (double)P;
     const bool sq = j >= 6;
-    r = wave_pw_sum<kBigPwDepth>(P, [=](int i) {
+    r = wave_pw_sum<kBigPwDepth>(m, [=](int i) {
       const double x = src[i];
       const double d = x - mean;
       return sq ? d * d : x;
     }, L.pw);
   } else {
-    const uint8_t LDSP *src = (j & 1) ? L.mcomp : L.ccomp;
+    const uint8_t LDSP *src = ((j & 1) ? L.mcomp : L.ccomp) + o;
     const double mean = res[j - 6] / (double)n_ex;
-    r = wave_pw_sum<kBigPwDepth>(n_ex, [=](int i) {
+    r = wave_pw_sum<kBigPwDepth>(m, [=](int i) {
       const double d = cent[src[i]] - mean;
       return d * d;
     }, L.pw);
   }
   wsync();
-  if (lane_id() == 0) res[j] = r;
+  if (lane_id() == 0) *dst = r;
   wsync();
 }
 
 // The jobs of bit set `jobs` spread over the block's waves (all threads call
 // it; returns after a barrier). A sum past the register plan uses the LDS
 // plan, of which the carve holds one copy: those run on wave 0 in turn.
+// halves: a job with n > 128 runs as numpy's top-level split, pairwise(n) =
+// pairwise(n2) + pairwise(n - n2) with n2 = n/2 - (n/2) % 8, the two halves on
+// two waves and their sum formed by wave 0 after the barrier (so only wave 0
+// may read those results).
 __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &T, char LDSP *base,
-                                              uint32_t jobs, int k, int n_ex) {
+                                              BigShared &B, uint32_t jobs, int k, int n_ex,
+                                              bool halves) {
   const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  double LDSP *res = reinterpret_cast<double LDSP *>(base + p.off_stage);  // L.jobres
   int slot = 0;
+  uint32_t split = 0;
 #pragma unroll 1
   while (jobs) {
     const int j = __builtin_ctz(jobs);
     jobs &= jobs - 1;
     const int n = j < 2 ? k : (j >= 4 && j < 8) ? p.P : n_ex;
-    const int w = n > pw_reg_cap(kBigPwDepth) ? 0 : (slot++ % nwv);
-    if (w == wid) big_sum_job(p, T, base, j, k, n_ex);
+    const bool two = halves && n > 128;
+    const int n2 = (n / 2) - (n / 2) % 8;
+#pragma unroll 1
+    for (int h = 0; h < (two ? 2 : 1); h++) {
+      const int o = two && h ? n2 : 0, m = two ? (h ? n - n2 : n2) : n;
+      const int w = m > pw_reg_cap(kBigPwDepth) ? 0 : (slot++ % nwv);
+      double LDSP *dst = two ? (double LDSP *)&B.half[2 * j + h] : res + j;
+      if (w == wid) big_sum_job(p, T, base, j, n_ex, o, m, dst);
+    }
+    if (two) split |= 1u << j;
   }
   __syncthreads();
+  if (split && wid == 0) {
+    if (lane_id() == 0)
+      for (uint32_t s = split; s; s &= s - 1) {
+        const int j = __builtin_ctz(s);
+        res[j] = B.half[2 * j] + B.half[2 * j + 1];
+      }
+    wsync();
+  }
 }
 
 // Wave 0 of k_env_big after the sums: reward, counters and termination.
@@ -2646,9 +2672,15 @@ VMP_SLOOP
       const int ws = nj < nwv ? nj : 0;
       if ((t >> 6) >= ws) big_store_obs(p, L, T, W, out_obs, t - 64 * ws, NT - 64 * ws);
     }
-    if (ja) big_sum_phase(p, T, L.base, ja, (int)k, n_ex);
+#ifndef VMP_ABL_NOA  // timing ablations only (rewards wrong): -DVMP_ABL_NOA / -DVMP_ABL_NOB
+    if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, false);
+#else
+    __syncthreads();
+#endif
     STAMP(20);
-    if (kl) big_sum_phase(p, T, L.base, 0x3C0u, (int)k, n_ex);
+#ifndef VMP_ABL_NOB
+    if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true);
+#endif
     STAMP(21);
   }
   if (w0) big_stats_final(p, B, L.base, k, n_ex, n_w, n_term, arrivals);
