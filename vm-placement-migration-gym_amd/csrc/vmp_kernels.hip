@@ -2338,7 +2338,14 @@ VMP_SLOOP
 // deviations; 8,9 VM-size squared deviations), each by one whole wave in
 // numpy's pairwise order. Out of line so its temporaries do not share the
 // register budget with the block's slot arrays.
-constexpr int kBigPwDepth = 6;  // register plan up to n = 7688
+#ifndef VMP_BIG_PW_DEPTH
+#define VMP_BIG_PW_DEPTH 6
+#endif
+#ifndef VMP_BIG_SPLIT_A
+#define VMP_BIG_SPLIT_A 0
+#endif
+constexpr int kBigPwDepth = VMP_BIG_PW_DEPTH;  // register plan up to n = 7688 (6), 1928 (4)
+constexpr bool kBigSplitA = VMP_BIG_SPLIT_A;   // split phase A's long sums too
 // Job j over elements [o, o + m) of its source (the whole job: o = 0, m = n),
 // result to *dst.
 __device__ VMP_BIG_CALL void big_sum_job(const EnvParams &p, const Tables &T, char LDSP *base,
@@ -2380,9 +2387,21 @@ __device__ VMP_BIG_CALL void big_sum_job(const EnvParams &p, const Tables &T, ch
 // pairwise(n2) + pairwise(n - n2) with n2 = n/2 - (n/2) % 8, the two halves on
 // two waves and their sum formed by wave 0 after the barrier (so only wave 0
 // may read those results).
+__device__ __forceinline__ int big_sum_n(const EnvParams &p, int j, int k, int n_ex) {
+  return j < 2 ? k : (j >= 4 && j < 8) ? p.P : n_ex;
+}
+// Number of wave tasks big_sum_phase deals for `jobs`.
+__device__ __forceinline__ int big_sum_ntask(const EnvParams &p, uint32_t jobs, int k, int n_ex,
+                                             bool halves) {
+  int n = 0;
+  for (; jobs; jobs &= jobs - 1) n += (halves && big_sum_n(p, __builtin_ctz(jobs), k, n_ex) > 128) ? 2 : 1;
+  return n;
+}
+// block_combine: the split results are formed before a block barrier (every
+// wave may read them), else by wave 0 alone after it.
 __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &T, char LDSP *base,
                                               BigShared &B, uint32_t jobs, int k, int n_ex,
-                                              bool halves) {
+                                              bool halves, bool block_combine) {
   const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   double LDSP *res = reinterpret_cast<double LDSP *>(base + p.off_stage);  // L.jobres
   int slot = 0;
@@ -2391,7 +2410,7 @@ __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &
   while (jobs) {
     const int j = __builtin_ctz(jobs);
     jobs &= jobs - 1;
-    const int n = j < 2 ? k : (j >= 4 && j < 8) ? p.P : n_ex;
+    const int n = big_sum_n(p, j, k, n_ex);
     const bool two = halves && n > 128;
     const int n2 = (n / 2) - (n / 2) % 8;
 #pragma unroll 1
@@ -2412,6 +2431,7 @@ __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &
       }
     wsync();
   }
+  if (split && block_combine) __syncthreads();
 }
 
 // Wave 0 of k_env_big after the sums: reward, counters and termination.
@@ -2665,21 +2685,21 @@ VMP_SLOOP
   STAMP(11);
   {  // phase A: plain sums; phase B (kl): squared deviations about their means
     const uint32_t ja = (k > 0 ? 0x3u : 0u) | (kl ? 0xCu : 0u) | (p.reward >= 1 ? 0x30u : 0u);
-    // the observation is written by the waves that get no phase-A sum (job i
-    // runs on wave i), so its stores drain while the sums run
-    const int nwv = NT >> 6, nj = __popc(ja);
+    // the observation is written by the waves that get no phase-A sum task
+    // (task i runs on wave i), so its stores drain while the sums run
+    const int nwv = NT >> 6, nj = big_sum_ntask(p, ja, (int)k, n_ex, kBigSplitA);
     if (out_obs) {
       const int ws = nj < nwv ? nj : 0;
       if ((t >> 6) >= ws) big_store_obs(p, L, T, W, out_obs, t - 64 * ws, NT - 64 * ws);
     }
 #ifndef VMP_ABL_NOA  // timing ablations only (rewards wrong): -DVMP_ABL_NOA / -DVMP_ABL_NOB
-    if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, false);
+    if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, kBigSplitA, true);
 #else
     __syncthreads();
 #endif
     STAMP(20);
 #ifndef VMP_ABL_NOB
-    if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true);
+    if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true, false);
 #endif
     STAMP(21);
   }
