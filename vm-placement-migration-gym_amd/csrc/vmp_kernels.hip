@@ -32,11 +32,22 @@
 
 namespace vmp {
 
+// Global (address space 1) views of HBM pointers. Pointers read out of the
+// EnvParams / StepOut structs are generic, and generic accesses compile to
+// FLAT instructions, which count in lgkmcnt as well as vmcnt: every later
+// s_waitcnt lgkmcnt for an LDS access then also waits for them to complete
+// (in k_env_big the mid-step state stores stalled every following LDS wait).
+#define GLBP __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ T GLBP *gptr(T *p) {
+  return (T GLBP *)p;
+}
+
 // Streaming stores (obs / state written once per launch, not re-read by it).
 #ifdef VMP_NT_STORE
-#define ST_NT(ptr, val) __builtin_nontemporal_store((val), (ptr))
+#define ST_NT(ptr, val) __builtin_nontemporal_store((val), gptr(ptr))
 #else
-#define ST_NT(ptr, val) (*(ptr) = (val))
+#define ST_NT(ptr, val) (*gptr(ptr) = (val))
 #endif
 
 // ------------------------------------------------------------ wave utils --
@@ -180,7 +191,7 @@ __device__ __noinline__ double loggam_far(double x) { return loggam_dev(x); }
 __device__ __forceinline__ bool ptrs_accept(double V, double us, int64_t k, double lam, double a,
                                          double b, double loglam, double log_invalpha,
                                          const double *tab, int tab_n) {
-  const double lg = (k + 1 < tab_n) ? tab[k + 1] : loggam_far((double)(k + 1));
+  const double lg = (k + 1 < tab_n) ? gptr(tab)[k + 1] : loggam_far((double)(k + 1));
   return (log(V) + log_invalpha - log(a / (us * us) + b)) <= (-lam + k * loglam - lg);
 }
 
@@ -1690,15 +1701,15 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
   // whose latency the random draws below overlap ----
   // (indices are clamped instead of branched on, so no load is conditional and
   // the waits below can count: a skipped load would force vmcnt(0))
-  const uint64_t hv = reinterpret_cast<const uint64_t *>(p.hdr + e)[lane & 31];
+  const uint64_t hv = gptr(reinterpret_cast<const uint64_t *>(p.hdr + e))[lane & 31];
   // Poisson constants for the block's LDS copy (issued before the state loads,
   // so waiting for them never waits on the state)
   constexpr int kPoisWords = (int)(2 * sizeof(PoisConst) / 4);
-  const uint32_t pw = reinterpret_cast<const uint32_t *>(p.pois)[threadIdx.x % kPoisWords];
+  const uint32_t pw = gptr(reinterpret_cast<const uint32_t *>(p.pois))[threadIdx.x % kPoisWords];
   // this lane's PCG64 jump entry (lane-parallel draws), right behind the header
   U128 JA{0, 0}, JM{0, 0};
   if (o.k_steps > 0) {
-    const uint64_t *jt = p.jump + 4 * lane;
+    const uint64_t GLBP *jt = gptr(p.jump + 4 * lane);
     JA = U128{jt[0], jt[1]};
     JM = U128{jt[2], jt[3]};
   }
@@ -1775,7 +1786,7 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
     }
     wsync();
     const double r = env_tail<VPT>(p, L, T, wa, rem, k, term STAMP_ARGS);
-    if (o.reward && lane == 0) o.reward[(int64_t)k * p.N + e] = r;
+    if (o.reward && lane == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
   if (o.k_steps > 0) svc_commit(L);
@@ -1791,8 +1802,8 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
   if (o.mask_bits) write_mask<VPT>(p, L, T, wa, o.mask_bits + (int64_t)e * V * p.W32);
   STAMP(5);
   if (o.k_steps > 0) {
-    if (o.done && lane == 0) o.done[e] = (uint8_t)term;
-    if (o.done_count && lane == 0) o.done_count[e] += ndone;
+    if (o.done && lane == 0) gptr(o.done)[e] = (uint8_t)term;
+    if (o.done_count && lane == 0) gptr(o.done_count)[e] += ndone;
     uint64_t *vmo = p.vmw + (int64_t)e * V;
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
@@ -1802,7 +1813,7 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
     double *pmo = p.pm + (int64_t)e * 2 * P;
     for (int i = lane; i < 2 * P; i += 64) ST_NT(pmo + i, (double)L.cpu[i]);
     if (lane < 32)
-      reinterpret_cast<uint64_t *>(p.hdr + e)[lane] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane];
+      gptr(reinterpret_cast<uint64_t *>(p.hdr + e))[lane] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane];
   }
   STAMP(6);
 #ifdef VMP_STAMPS
@@ -2495,7 +2506,8 @@ __device__ VMP_BIG_CALL void big_stats_final(const EnvParams &p, BigShared &B, c
 __device__ VMP_BIG_CALL void big_predraw(const EnvParams &p, const Tables &T, char LDSP *base,
                                          int K, const uint64_t *jt) {
   const Lds L = make_lds(p, base);
-  const U128 JA{jt[0], jt[1]}, JM{jt[2], jt[3]};
+  const uint64_t GLBP *g = gptr(jt);
+  const U128 JA{g[0], g[1]}, JM{g[2], g[3]};
   predraw(p, L, T, K, p.V, JA, JM);
 }
 
@@ -2735,17 +2747,17 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
     T.fcent[i] = (float)((double)i / 100.0);
   }
   constexpr int kPoisWords = (int)(2 * sizeof(PoisConst) / 4);
-  if (t < kPoisWords) reinterpret_cast<uint32_t *>(T.pois)[t] = reinterpret_cast<const uint32_t *>(p.pois)[t];
+  if (t < kPoisWords) reinterpret_cast<uint32_t *>(T.pois)[t] = gptr(reinterpret_cast<const uint32_t *>(p.pois))[t];
   // every global load of the env's state is issued before the first LDS store
   // (indices clamped, not branched on, so the loads are unconditional):
   // header, the first 4*NT PM words, the VM words
-  const uint64_t hv = reinterpret_cast<const uint64_t *>(p.hdr + e)[t & 31];
-  const double *pm = p.pm + (int64_t)e * 2 * P;
+  const uint64_t hv = gptr(reinterpret_cast<const uint64_t *>(p.hdr + e))[t & 31];
+  const double GLBP *pm = gptr(p.pm + (int64_t)e * 2 * P);
   const int n_pm = 2 * P;
   double pv[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) pv[j] = pm[min(j * NT + t, n_pm - 1)];
-  const uint64_t *vmw = p.vmw + (int64_t)e * V;
+  const uint64_t GLBP *vmw = gptr(p.vmw + (int64_t)e * V);
   uint64_t wv[SPT];
 #pragma unroll
   for (int s = 0; s < SPT; s++) wv[s] = vmw[min(s * NT + t, V - 1)];
@@ -2795,7 +2807,7 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
     const double r = big_tail<SPT>(p, L, T, B, W, rem, k, term,
                                    last && o.obs ? o.obs + (int64_t)e * p.D : nullptr, last, e
                                    STAMP_ARGS);
-    if (o.reward && t == 0) o.reward[(int64_t)k * p.N + e] = r;
+    if (o.reward && t == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
   if (o.k_steps > 0) {
@@ -2840,10 +2852,10 @@ VMP_SLOOP
     }
   }
   if (o.k_steps > 0) {
-    if (o.done && t == 0) o.done[e] = (uint8_t)term;
-    if (o.done_count && t == 0) o.done_count[e] += ndone;
+    if (o.done && t == 0) gptr(o.done)[e] = (uint8_t)term;
+    if (o.done_count && t == 0) gptr(o.done_count)[e] += ndone;
     if (t < 32)
-      reinterpret_cast<uint64_t *>(p.hdr + e)[t] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
+      gptr(reinterpret_cast<uint64_t *>(p.hdr + e))[t] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
   }
   STAMP(6);
   STAMP_FLUSH();
