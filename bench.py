@@ -37,12 +37,23 @@ CFG = dict(pms=100, vms=1000, arrival_rate=1.8182, service_length=1000, training
            cap_target_util=True, beta=0.5, allow_null_action=True)
 
 
-def step_bytes(P, V):
+def step_bytes(P, V, words):
     """Algorithmic HBM bytes per env-step of the per-step kernel:
-    state read + write (8 B/VM word, 16 B/PM, 256 B header), obs f32[3V+2P],
-    reward f64, done u8."""
+    state read (8 B/VM word, 16 B/PM, 256 B header), obs f32[3V+2P], PM and
+    header write, reward f64, done u8, and the VM words that changed (`words`
+    per env-step: a running VM's word holds its finish key and is not rewritten
+    while it runs)."""
     state = 8 * V + 16 * P + 256
-    return 2 * state + 4 * (3 * V + 2 * P) + 8 + 1
+    return state + 4 * (3 * V + 2 * P) + 16 * P + 256 + 8 + 1 + 8 * words
+
+
+def changed_words(c0, c1, env_steps):
+    """VM words written per env-step between two counter snapshots
+    ([total_requests, served, suspend, place, dropped, timestep] per env):
+    accepted arrivals + finishers + placements + suspensions. An upper bound:
+    a slot freed and refilled in the same step is written once, counted twice."""
+    d = (c1 - c0).double().sum(0)
+    return float((d[0] - d[4] + d[1] + d[2] + d[3]) / env_steps)
 
 
 def main():
@@ -118,23 +129,28 @@ def main():
     torch.cuda.synchronize(dev)
 
     # ---- timed region: exactly K steps, barrier + sync on both sides ----
+    # (one HIP event pair on the launch stream brackets the K launches: the
+    # average launch duration includes the gaps between back-to-back kernels,
+    # so it is an upper bound of rocprofv3's per-dispatch average)
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    c_before = env.counters()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(K):
-        ev[i][0].record(stream)
         one_step()
-        ev[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    words = changed_words(c_before, env.counters(), N * K)  # after the clock stops
+    kern_ms = ev0.elapsed_time(ev1) / K
     if dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -211,7 +227,7 @@ def main():
                    "sample": f"{n_cpu} envs x {steps_cpu} FirstFit act+step after {warm_cpu} "
                              f"warm-up steps, OpenMP {threads} threads (C oracle, same config)"}
 
-    bpe = step_bytes(P, V)
+    bpe = step_bytes(P, V, words)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
@@ -242,7 +258,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "vmp::k_env<16, true> (heuristic act+step, one step per launch)", "kernel_ms": kern_ms,
-                     "bytes_per_env_step": bpe},
+                     "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words},
         "cpu_baseline": cpu,
         "reference_cpu": _reference_cpu(),
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},
@@ -353,28 +369,30 @@ def bench_stress(args, dev, rank, world, dist):
     if dist:
         dist.barrier()
     K = args.stress_steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c_before = env.counters()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
+    ev0.record(stream)
+    for _ in range(K):
         _lib.check(L.vmp_heuristic_step(h, 1, None, _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done),
                                         None))
-        b.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
-    kern_ms = _max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in ev])), dev, dist)
+    words = changed_words(c_before, env.counters(), N * K)
+    kern_ms = _max_over_ranks(ev0.elapsed_time(ev1) / K, dev, dist)
     env.close()
-    bpe = step_bytes(P, V)
+    bpe = step_bytes(P, V, words)
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
             "workload": "P1000 V10000, lambda 1.818, L 1000, reward kl, BestFit act + step "
                         "(k_env_big, one workgroup per env)", "envs_per_gpu": N,
             "ff_steps": args.stress_ff, "steps": K, "mean_running": running,
             "mean_waiting": waiting, "ms_per_step": 1e3 * el / K, "kernel_ms": kern_ms,
-            "bytes_per_env_step": bpe,
+            "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "kernel": "vmp::k_env_big<20, true>"}}
 
@@ -413,6 +431,7 @@ def bench_external(args, env, dev, stream, dist, world, P, V):
     K = args.ext_steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(K)]
+    c_before = env.counters()
     t0 = time.perf_counter()
     for a, b in ev:
         one(a, b)
@@ -420,13 +439,14 @@ def bench_external(args, env, dev, stream, dist, world, P, V):
     if dist:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    words = changed_words(c_before, env.counters(), N * K)
     kern_ms = _max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in ev])), dev, dist)
-    bpe = step_bytes(P, V) + 4 * V
+    bpe = step_bytes(P, V, words) + 4 * V
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     return {"value": world * N / (kern_ms * 1e-3), "unit": "env-steps/s",
             "value_kind": "step kernel alone (events around vmp_step)",
             "act_plus_step_wall": world * N * K / el, "steps": K, "kernel_ms": kern_ms,
-            "bytes_per_env_step": bpe,
+            "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS,
                          "kernel": "vmp::k_env<16, true> (external actions)"}}

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Full GPU check: the whole -m gpu suite, smoke(), then the default bench line.
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "tests_rc=$rc"; tail -3 gpurun_out/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke_rc=$rc"; tail -2 gpurun_out/smoke.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench_rc=$rc"; [ $rc -ne 0 ] && exit $rc
+python - <<'PY'
+import json
+d = json.loads(open("gpurun_out/bench.log").read().strip().splitlines()[-1])
+r = d["roofline"]
+print("headline", round(d["value"] / 1e6, 2), "M/s ms_per_step", round(d["ms_per_step"], 4), "kern_ms", round(r["kernel_ms"], 4), "frac", round(r["frac"], 4), "B", round(r["bytes_per_env_step"]), "words", r.get("vm_words_written_per_env_step"))
+print("parity", d["parity"], "cpu", (d.get("cpu_baseline") or {}).get("value"))
+for k in ("external_actions", "stress_p1000_v10000", "fused_rollout", "ppo_train", "ppo_train_bf16", "ppo_eval"):
+    x = d.get(k)
+    if isinstance(x, dict):
+        print(k, {kk: (round(v, 4) if isinstance(v, float) else v) for kk, v in x.items() if kk in ("value", "kernel_ms", "bytes_per_env_step", "vm_words_written_per_env_step", "mean_running", "mean_waiting", "s_per_update", "error")}, x.get("roofline", {}).get("frac"))
+PY
+exit 0

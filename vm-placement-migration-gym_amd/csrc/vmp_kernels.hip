@@ -27,7 +27,7 @@
 #define VMP_WAVES_PER_EU 2
 #endif
 #ifndef VMP_WAVES_PER_EU_ONE  // the per-step (k_steps == 1) instantiation
-#define VMP_WAVES_PER_EU_ONE 2
+#define VMP_WAVES_PER_EU_ONE 3
 #endif
 
 namespace vmp {
@@ -1423,20 +1423,38 @@ __device__ __forceinline__ double kl_reward(double tcm, double tmm, double tcv, 
 
 // Everything of step() after the action phase: _run_vms, _accept_vm_requests,
 // stats + reward, termination (env.py:101, 108-163, 244-293).
-template <int VPT>
+// LAZY (the per-step launch): the high words are not held in registers. `fb`
+// bit s says whether slot s finishes this step if it runs (running: F - t <= 1;
+// waiting: remaining <= 1, i.e. placed now it finishes now), accepted words are
+// stored at once through `vmo`, and the caller fixes the finish keys of placed /
+// suspended VMs in memory; rem[] is then unused.
+template <int VPT, bool LAZY>
 __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, const Tables &T,
                                            uint32_t (&wa)[VPT], uint32_t (&rem)[VPT],
-                                           int kstep, bool &terminated STAMP_PARAMS) {
+                                           uint32_t run0, uint32_t fb, uint32_t &dirty,
+                                           uint64_t *vmo, int kstep,
+                                           bool &terminated STAMP_PARAMS) {
   const int lane = lane_id();
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
   EnvHdr LDSP *H = L.hdr;
   // ---- _run_vms (env.py:244-268) ----
+  // A running VM's word holds its finish key F = t + remaining (t = this
+  // step's timestep), so the per-step decrement of every running VM is implicit
+  // and its word is not rewritten; waiting VMs hold the remaining runtime
+  // itself. The action phase only moves VMs between WAIT and a PM (external
+  // migrations PM -> PM' are invalid, env.py:35-44), so run0 (running before the
+  // action phase) tells which words switch representation.
+  const uint32_t t32 = (uint32_t)H->timestep;
   int64_t n_term = 0;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const bool running = w_pl(wa[s]) < P;
-    if (running && rem[s] > 0) rem[s] -= 1;
-    const bool term = running && rem[s] == 0;
+    if (running != (bool)((run0 >> s) & 1u)) {
+      if (!LAZY) rem[s] = running ? rem[s] + t32 : rem[s] - t32;  // placed : suspended
+      dirty |= 1u << s;
+    }
+    // remaining r = F - t: decrement if r > 0, finish if it reaches 0
+    const bool term = running && (LAZY ? (bool)((fb >> s) & 1u) : (int32_t)(rem[s] - t32) <= 1);
     uint64_t it = ballot(term);
     n_term += __popcll(it);
     const uint32_t me = wa[s];
@@ -1457,7 +1475,8 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     }
     if (term) {
       wa[s] = w_make(NUL, 0, 0);
-      rem[s] = 0;
+      if (!LAZY) rem[s] = 0;
+      dirty |= 1u << s;
     }
   }
   for (int i = lane; i < P; i += 64) {  // precision clamp (env.py:267-268)
@@ -1493,7 +1512,13 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
         for (int s = 0; s < VPT; s++)
           if (s == (v >> 6)) {
             wa[s] = w_make(WAIT, cc, cm);
-            rem[s] = rr;
+            if (LAZY) {  // final for this launch: stored now, skipped at the end
+              ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rr << 32));
+              dirty &= ~(1u << s);
+            } else {
+              rem[s] = rr;
+              dirty |= 1u << s;
+            }
           }
       }
       if (lane == 0) {
@@ -1720,14 +1745,23 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
   for (int j = 0; j < 4; j++) pv[j] = pm[min(j * 64 + lane, n_pm - 1)];
   __asm__ volatile("" ::: "memory");  // keep the issue order: header/PM first
   const uint64_t *vmw = p.vmw + (int64_t)e * V;
+  // ONE: only the low halves (placement, sizes) go to registers here; the
+  // finish keys are read after the draws and folded into one bit per slot
+  const uint32_t GLBP *vlo = gptr(reinterpret_cast<const uint32_t *>(vmw));
   uint32_t wa[VPT], rem[VPT];
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
-    const uint64_t x = vmw[min(v, V - 1)];
-    const uint64_t w = v < V ? x : (uint64_t)kPad;
-    wa[s] = (uint32_t)w;
-    rem[s] = (uint32_t)(w >> 32);
+    if (ONE) {
+      const uint32_t x = vlo[2 * min(v, V - 1)];
+      wa[s] = v < V ? x : (uint32_t)kPad;
+      rem[s] = 0;
+    } else {
+      const uint64_t x = vmw[min(v, V - 1)];
+      const uint64_t w = v < V ? x : (uint64_t)kPad;
+      wa[s] = (uint32_t)w;
+      rem[s] = (uint32_t)(w >> 32);
+    }
   }
   __asm__ volatile("" ::: "memory");  // ... and the VM words before any wait
   // size tables (k/100 in f64 and f32) while the loads are in flight; the only
@@ -1767,6 +1801,16 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
 #endif
   bool term = false;
   int64_t ndone = 0;
+  uint32_t dirty = 0;  // bit s: this lane's VM word s changed (stored at the end)
+  uint32_t fb = 0;     // ONE: bit s = slot s finishes this step if it runs
+  uint32_t hiv[VPT];   // ONE: the finish keys / remaining runtimes, in flight
+  if (ONE) {
+    // issued before the action phase, consumed after it (latency hidden by it)
+#pragma unroll
+    for (int s = 0; s < VPT; s++) hiv[s] = vlo[2 * min(s * 64 + lane, V - 1) + 1];
+    __asm__ volatile("" ::: "memory");
+  }
+  uint64_t *vmo = p.vmw + (int64_t)e * V;
   const int k_steps = ONE ? 1 : o.k_steps;
 #pragma unroll 1
   for (int k = 0; k < k_steps; k++) {
@@ -1774,18 +1818,30 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
     uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
     int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
     int64_t n_place = 0, n_susp = 0;
+    uint32_t run0 = 0;
+#pragma unroll
+    for (int s = 0; s < VPT; s++) run0 |= (uint32_t)(w_pl(wa[s]) < P) << s;
     if (o.policy >= 0)
       n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row STAMP_ARGS);
     else
       external_apply<VPT>(p, L, T, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
     STAMP(1);
+    if (ONE) {
+      const uint32_t t32 = (uint32_t)L.hdr->timestep;
+#pragma unroll
+      for (int s = 0; s < VPT; s++) {  // by the placement before the action phase
+        const bool was_run = (run0 >> s) & 1u;
+        const bool f = was_run ? (int32_t)(hiv[s] - t32) <= 1 : hiv[s] <= 1u;
+        fb |= (uint32_t)f << s;
+      }
+    }
     wsync();
     if (lane == 0) {
       L.hdr->place_action += n_place;
       L.hdr->suspend_action += n_susp;
     }
     wsync();
-    const double r = env_tail<VPT>(p, L, T, wa, rem, k, term STAMP_ARGS);
+    const double r = env_tail<VPT, ONE>(p, L, T, wa, rem, run0, fb, dirty, vmo, k, term STAMP_ARGS);
     if (o.reward && lane == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
@@ -1804,11 +1860,22 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
   if (o.k_steps > 0) {
     if (o.done && lane == 0) gptr(o.done)[e] = (uint8_t)term;
     if (o.done_count && lane == 0) gptr(o.done_count)[e] += ndone;
-    uint64_t *vmo = p.vmw + (int64_t)e * V;
+    const uint32_t t32 = (uint32_t)(L.hdr->timestep - 1);  // this launch's step
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
       const int v = s * 64 + lane;
-      if (live(wa[s])) ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rem[s] << 32));
+      if (live(wa[s]) && ((dirty >> s) & 1u)) {  // unchanged words stay as they are
+        if (!ONE) {
+          ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rem[s] << 32));
+        } else if (w_pl(wa[s]) == P + 1) {  // finished: NULL, remaining 0
+          ST_NT(vmo + v, (uint64_t)wa[s]);
+        } else {  // placed (r -> F = t + r) or suspended (F -> r = F - t)
+          uint32_t GLBP *w32 = gptr(reinterpret_cast<uint32_t *>(vmo + v));
+          w32[0] = wa[s];
+          __hip_atomic_fetch_add(w32 + 1, w_pl(wa[s]) < P ? t32 : 0u - t32, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
     double *pmo = p.pm + (int64_t)e * 2 * P;
     for (int i = lane; i < 2 * P; i += 64) ST_NT(pmo + i, (double)L.cpu[i]);
@@ -1889,7 +1956,10 @@ __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double
     if (placement) placement[i] = (int64_t)(w & 0xFFFF);
     if (vm_cpu) vm_cpu[i] = (double)((w >> 16) & 0xFF) / 100.0;
     if (vm_mem) vm_mem[i] = (double)((w >> 24) & 0xFF) / 100.0;
-    if (remaining) remaining[i] = (int64_t)(w >> 32);
+    if (remaining) {  // running VMs hold their finish key F = timestep + remaining
+      const int64_t hi = (int64_t)(w >> 32);
+      remaining[i] = (int)(w & 0xFFFF) < p.P ? (int64_t)(uint32_t)((uint32_t)hi - (uint32_t)p.hdr[i / p.V].timestep) : hi;
+    }
   }
   int64_t np_ = (int64_t)p.N * p.P;
   if (i < np_) {
@@ -2518,7 +2588,7 @@ __device__ VMP_BIG_CALL void big_predraw(const EnvParams &p, const Tables &T, ch
 template <int SPT>
 __device__ __forceinline__ void big_store(const EnvParams &p, const Lds &L, const Tables &T,
                                           const uint32_t LDSP *W, const uint32_t (&rem)[SPT],
-                                          float *obs, bool state, int e) {
+                                          uint32_t dirty, float *obs, bool state, int e) {
   const int t = threadIdx.x, NT = blockDim.x;
   const int V = p.V, P = p.P;
   uint64_t *vmo = p.vmw + (int64_t)e * V;
@@ -2532,7 +2602,7 @@ __device__ __forceinline__ void big_store(const EnvParams &p, const Lds &L, cons
         ST_NT(obs + V + v, T.fcent[w_cc(w)]);
         ST_NT(obs + 2 * V + v, T.fcent[w_cm(w)]);
       }
-      if (state) ST_NT(vmo + v, (uint64_t)w | ((uint64_t)rem[s] << 32));
+      if (state && ((dirty >> s) & 1u)) ST_NT(vmo + v, (uint64_t)w | ((uint64_t)rem[s] << 32));
     }
   }
   if (obs)
@@ -2570,21 +2640,29 @@ __device__ __forceinline__ void big_store_obs(const EnvParams &p, const Lds &L, 
 template <int SPT>
 __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, const Tables &T,
                                            BigShared &B, uint32_t LDSP *W,
-                                           uint32_t (&rem)[SPT], int kstep,
-                                           bool &terminated, float *out_obs, bool store_state,
-                                           int e STAMP_PARAMS) {
+                                           uint32_t (&rem)[SPT], uint32_t run0, uint32_t &dirty,
+                                           int kstep, bool &terminated, float *out_obs,
+                                           bool store_state, int e STAMP_PARAMS) {
   const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
   EnvHdr LDSP *H = L.hdr;
-  // ---- _run_vms: decrement, then free the finishers in ascending VM order ----
+  // ---- _run_vms: finish keys (env_tail), then free the finishers in ascending VM order ----
+  const uint32_t t32 = (uint32_t)H->timestep;
   uint32_t fterm = 0;
 #pragma unroll
   for (int s = 0; s < SPT; s++) {  // rem[] statically indexed: stays in registers
     const bool running = w_pl(W[s * NT + t]) < P;
-    if (running && rem[s] > 0) rem[s] -= 1;
-    if (running && rem[s] == 0) fterm |= 1u << s;
+    if (running != (bool)((run0 >> s) & 1u)) {
+      rem[s] = running ? rem[s] + t32 : rem[s] - t32;
+      dirty |= 1u << s;
+    }
+    if (running && (int32_t)(rem[s] - t32) <= 1) {
+      fterm |= 1u << s;
+      rem[s] = 0;  // the word becomes NULL (below)
+    }
   }
+  dirty |= fterm;
   const int n_term = row_counts<SPT>(fterm, B);
 #pragma unroll 1
   for (int j0 = 0; j0 < n_term; j0 += 512) {
@@ -2656,6 +2734,7 @@ VMP_SLOOP
         if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
           W[s * NT + t] = w_make(WAIT, L.accc[j], L.accm[j]);
           rem[s] = (uint32_t)B.evt[j - j0];
+          dirty |= 1u << s;
         }
       }
       __syncthreads();
@@ -2667,7 +2746,7 @@ VMP_SLOOP
   }
   __syncthreads();
   // the VM words and PM resources are final: their owners store them now
-  if (store_state) big_store<SPT>(p, L, T, W, rem, nullptr, true, e);
+  if (store_state) big_store<SPT>(p, L, T, W, rem, dirty, nullptr, true, e);
   STAMP(3);
   // ---- stats + reward ----
   const bool kl = p.reward == 2;
@@ -2786,6 +2865,7 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   STAMP(13);
   bool term = false;
   int64_t ndone = 0;
+  uint32_t dirty = 0;  // bit s: this thread's VM word s changed (stored by big_store)
   const int k_steps = ONE ? 1 : o.k_steps;
 #pragma unroll 1
   for (int k = 0; k < k_steps; k++) {
@@ -2793,6 +2873,9 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
     uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
     int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
     int64_t n_place = 0, n_susp = 0;
+    uint32_t run0 = 0;
+VMP_SLOOP
+    for (int s = 0; s < SPT; s++) run0 |= (uint32_t)(w_pl(W[s * NT + t]) < P) << s;
     if (o.policy >= 0)
       n_place = big_heuristic<SPT>(p, L, T, B, W, o.policy, act_row, valid_row STAMP_ARGS);
     else
@@ -2804,7 +2887,7 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
       L.hdr->suspend_action += n_susp;
     }
     __syncthreads();
-    const double r = big_tail<SPT>(p, L, T, B, W, rem, k, term,
+    const double r = big_tail<SPT>(p, L, T, B, W, rem, run0, dirty, k, term,
                                    last && o.obs ? o.obs + (int64_t)e * p.D : nullptr, last, e
                                    STAMP_ARGS);
     if (o.reward && t == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
@@ -2821,7 +2904,7 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   __syncthreads();
   STAMP(4);
   // a stepping launch stored obs and state after its last accept phase
-  if (o.obs && o.k_steps == 0) big_store<SPT>(p, L, T, W, rem, o.obs + (int64_t)e * p.D, false, e);
+  if (o.obs && o.k_steps == 0) big_store<SPT>(p, L, T, W, rem, 0u, o.obs + (int64_t)e * p.D, false, e);
   if (o.mask_bits) {
     uint32_t *bits = o.mask_bits + (int64_t)e * V * p.W32;
     const int A = p.A, NW32 = p.W32, WAIT = p.P, NUL = p.P + 1;

@@ -9,7 +9,11 @@
 //                       bits 16..23 vm_cpu in hundredths (np.around(.,2) makes
 //                                   every size k/100 exactly, env.py:212-219)
 //                       bits 24..31 vm_memory in hundredths
-//                       bits 32..63 remaining runtime (env.py:290)
+//                       bits 32..63 waiting VM: remaining runtime (env.py:290);
+//                                   running VM: finish key F = timestep +
+//                                   remaining, so a running VM's word does not
+//                                   change while it runs (the step kernels
+//                                   store only the words that changed)
 //   pm   f64 [N][2][P] cpu[P] then memory[P]; kept in f64 because their values
 //                       carry the reference's accumulated rounding history
 //   hdr  EnvHdr [N]    256 B: 4 PCG64 streams, sequence bases, counters, stats
