@@ -449,7 +449,7 @@ def bench_external(args, env, dev, stream, dist, world, P, V):
             "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS,
-                         "kernel": "vmp::k_env<16, true> (external actions)"}}
+                         "kernel": "vmp::k_env_ext<16> (external actions)"}}
 
 
 def _reference_cpu():

@@ -18,6 +18,8 @@ namespace vmp {
 constexpr int kStamps = 24;  // per-env phase clocks (diagnostic builds)
 template <int VPT, bool ONE>
 __global__ void k_env(EnvParams p, StepOut o);
+template <int VPT>
+__global__ void k_env_ext(EnvParams p, StepOut o);
 template <int SPT, bool ONE>
 __global__ void k_env_big(EnvParams p, StepOut o);
 __global__ void k_rank(EnvParams p, int64_t *rank);
@@ -203,6 +205,15 @@ void carve(vmp_handle *h) {
   p.lds_wave_bytes = (int32_t)off;
 }
 
+void launch_ext(int need, dim3 grid, dim3 block, size_t lds, hipStream_t s, const EnvParams &p,
+                const StepOut &o) {
+  if (need <= 1) hipLaunchKernelGGL((k_env_ext<1>), grid, block, lds, s, p, o);
+  else if (need <= 2) hipLaunchKernelGGL((k_env_ext<2>), grid, block, lds, s, p, o);
+  else if (need <= 4) hipLaunchKernelGGL((k_env_ext<4>), grid, block, lds, s, p, o);
+  else if (need <= 8) hipLaunchKernelGGL((k_env_ext<8>), grid, block, lds, s, p, o);
+  else hipLaunchKernelGGL((k_env_ext<16>), grid, block, lds, s, p, o);
+}
+
 template <bool ONE>
 void launch_vpt(int need, dim3 grid, dim3 block, size_t lds, hipStream_t s, const EnvParams &p,
                 const StepOut &o) {
@@ -249,7 +260,10 @@ int launch_env(vmp_handle *h, const StepOut &o) {
     return VMP_OK;
   }
   const int need = (h->V + 63) / 64;
-  if (o.k_steps == 1) launch_vpt<true>(need, grid, block, lds, h->stream, p, o);
+  if (o.actions) {  // external actions: vmp_step, one step
+    if (o.k_steps != 1) return fail(VMP_EINVAL, "external actions take one step per launch");
+    launch_ext(need, grid, block, lds, h->stream, p, o);
+  } else if (o.k_steps == 1) launch_vpt<true>(need, grid, block, lds, h->stream, p, o);
   else launch_vpt<false>(need, grid, block, lds, h->stream, p, o);
   HIP_TRY(hipGetLastError());
   return VMP_OK;

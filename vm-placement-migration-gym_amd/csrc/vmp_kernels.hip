@@ -1293,7 +1293,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
             if (ok) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)q;
             else bad |= 1u << s;
           }
-        if (act_out) act_out[ws * 64 + wl] = q;
+        if (act_out) gptr(act_out)[ws * 64 + wl] = q;
       }
       // heuristic state update (f32): FF updates cpu only (firstfit.py:36)
       const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
@@ -1341,8 +1341,8 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     for (int s = 0; s < VPT; s++) {
       const int v = s * 64 + lane;
       if (live(wa[s])) {
-        if (act_out && !((won >> s) & 1u)) act_out[v] = (int32_t)w_pl(wa[s]);
-        if (valid_out) valid_out[v] = (uint8_t)!((bad >> s) & 1u);
+        if (act_out && !((won >> s) & 1u)) gptr(act_out)[v] = (int32_t)w_pl(wa[s]);
+        if (valid_out) gptr(valid_out)[v] = (uint8_t)!((bad >> s) & 1u);
       }
     }
   }
@@ -1359,12 +1359,19 @@ __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L,
                                                int64_t &n_susp) {
   const int lane = lane_id();
   const int P = p.P, WAIT = p.P;
+  // all action loads issued at once, unconditionally (clamped index) and
+  // through the global address space: one wait for all of them instead of a
+  // conditional load + wait per slot row
+  const int32_t GLBP *ar = gptr(act_row);
+  int32_t tv[VPT];
+#pragma unroll
+  for (int s = 0; s < VPT; s++) tv[s] = ar[min(s * 64 + lane, p.V - 1)];
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
     const bool in = live(wa[s]);
     const int c = w_pl(wa[s]);
-    const int t = in ? act_row[v] : c;
+    const int t = in ? tv[s] : c;
     const bool isplace = in && c == WAIT && t >= 0 && t < P;
     const bool issusp = in && c < P && t == WAIT;
     uint64_t evm = ballot(isplace || issusp);
@@ -1404,7 +1411,7 @@ __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L,
     n_place += __popcll(okm & ballot(isplace));
     n_susp += __popcll(ballot(issusp));
     if (ok && t != c && in) wa[s] = (wa[s] & 0xFFFF0000u) | (uint32_t)t;
-    if (valid_out && in) valid_out[v] = (uint8_t)ok;
+    if (valid_out && in) gptr(valid_out)[v] = (uint8_t)ok;
   }
 }
 
@@ -1706,8 +1713,10 @@ __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, con
 
 // ONE = true is the per-step launch (k_steps == 1, the Base.test loop body); it
 // is a separate instantiation so profiles tell it apart from fused rollouts.
-template <int VPT, bool ONE>
-__global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
+// EXT = true: the external-action step (vmp_step), its own kernel k_env_ext so
+// the heuristic's registers do not weigh on it and vice versa.
+template <int VPT, bool ONE, bool EXT>
+__device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   extern __shared__ __align__(16) char lds[];
   __shared__ Tables T;
 #ifdef VMP_STAMPS
@@ -1821,7 +1830,7 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
     uint32_t run0 = 0;
 #pragma unroll
     for (int s = 0; s < VPT; s++) run0 |= (uint32_t)(w_pl(wa[s]) < P) << s;
-    if (o.policy >= 0)
+    if (!EXT)
       n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row STAMP_ARGS);
     else
       external_apply<VPT>(p, L, T, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
@@ -1846,7 +1855,7 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
     ndone += term;
   }
   if (o.k_steps > 0) svc_commit(L);
-  if (o.k_steps == 0 && o.policy >= 0 && o.act_out) {
+  if (!EXT && o.k_steps == 0 && o.policy >= 0 && o.act_out) {
     // act only: decide on a scratch copy of the VM words; nothing is stored
     uint32_t wt[VPT];
 #pragma unroll
@@ -1892,6 +1901,20 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE 
   STAMP_FLUSH();
 }
 
+template <int VPT, bool ONE>
+__global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
+  env_body<VPT, ONE, false>(p, o);
+}
+template <int VPT>
+__global__ __launch_bounds__(64 * kEnvWavesPerBlock, VMP_WAVES_PER_EU_ONE) void k_env_ext(EnvParams p, StepOut o) {
+  env_body<VPT, true, true>(p, o);
+}
+
+template __global__ void k_env_ext<1>(EnvParams, StepOut);
+template __global__ void k_env_ext<2>(EnvParams, StepOut);
+template __global__ void k_env_ext<4>(EnvParams, StepOut);
+template __global__ void k_env_ext<8>(EnvParams, StepOut);
+template __global__ void k_env_ext<16>(EnvParams, StepOut);
 template __global__ void k_env<1, false>(EnvParams, StepOut);
 template __global__ void k_env<1, true>(EnvParams, StepOut);
 template __global__ void k_env<2, false>(EnvParams, StepOut);
