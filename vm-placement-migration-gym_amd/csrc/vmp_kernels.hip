@@ -825,6 +825,17 @@ __device__ __forceinline__ uint64_t prefix_or64(uint64_t x) {
   return ((uint64_t)prefix_or32((uint32_t)(x >> 32)) << 32) | prefix_or32((uint32_t)x);
 }
 
+// Inclusive prefix max across the wave for values >= 0 (0 is the identity).
+__device__ __forceinline__ uint32_t prefix_max32(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+  return x;
+}
+
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
@@ -871,6 +882,33 @@ __device__ __forceinline__ void build_bitmaps(const EnvParams &p, const Lds &L, 
       L.bm[rhi * NW + w] = m1;
     }
   }
+  wsync();
+}
+
+// Exact any-fit pre-check (the heuristics' common no-placement case): M[k] =
+// max of the +1-encoded memory thresholds tm over the PMs whose cpu threshold
+// is >= k (0: none). A VM of sizes (kc, km) fits some PM iff M[kc] > km, the
+// same predicate as "some fit bitmap bit is set" (firstfit.py:33,
+// bestfit.py:35: cpu and memory both fit). Rows reversed over the lanes as in
+// build_bitmaps, so the suffix max over k is a lane prefix max.
+__device__ __forceinline__ void build_fitmax(const EnvParams &p, const Lds &L, uint32_t LDSP *M) {
+  const int lane = lane_id();
+  M[lane] = 0;
+  M[lane + 64] = 0;
+  wsync();
+  for (int q = lane; q < p.P; q += 64) {
+    const int tcq = (int)L.tc[q];
+    if (tcq > 0) __atomic_fetch_max(&M[tcq - 1], (uint32_t)L.tm[q], __ATOMIC_RELAXED);
+  }
+  wsync();
+  const int rlo = 63 - lane, rhi = 127 - lane;
+  const bool hi_ok = rhi <= 100;
+  uint32_t c1 = hi_ok ? M[rhi] : 0u, c0 = M[rlo];
+  c1 = prefix_max32(c1);
+  c0 = max(prefix_max32(c0), (uint32_t)__builtin_amdgcn_readlane((int)c1, 63));
+  wsync();
+  M[rlo] = c0;
+  if (hi_ok) M[rhi] = c1;
   wsync();
 }
 
@@ -1230,10 +1268,18 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     }
     wsync();
     STAMP(16);
+    bool anyfit = false;
+    {  // the fit bitmaps are built only if some pending VM fits somewhere
+      uint32_t LDSP *M = reinterpret_cast<uint32_t LDSP *>(L.bc);
+      build_fitmax(p, L, M);
+#pragma unroll
+      for (int s = 0; s < VPT; s++)
+        anyfit |= ((pend >> s) & 1u) && M[w_cc(wa[s])] > (uint32_t)w_cm(wa[s]);
+    }
     bool rebuild = true;
     uint32_t hit = 0;  // bit s: VM slot s of this lane is pending and some PM fits it
 #pragma unroll 1
-    for (;;) {
+    for (; ballot(anyfit);) {
       if (rebuild) {  // single site: the initial build (index-order fit bitmaps)
         build_bitmaps(p, L, false);
         rebuild = false;
