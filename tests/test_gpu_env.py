@@ -339,3 +339,61 @@ def test_c5_steady_state_bestfit_kl_vs_oracle():
             assert np.array_equal(sd[k][i].cpu().numpy(), so[j]), (k, i)
         assert np.array_equal(ctr[i], e.counters()[0]), i
     b.close()
+
+
+def test_headline_steady_state_firstfit_vs_oracle():
+    """The bench workload (BASELINE headline: config/100.yml with vms = 1000,
+    L = 1000, reward wr, FirstFit, training mode) at its steady state: 256 envs
+    (seeds 4·i as bench.py's) fast-forwarded 2900 steps by the fused rollout,
+    whose rewards must equal the oracle's, then 200 per-step act+step launches
+    (k_env<16, true>) through the VMs placed in the refill burst finishing
+    (~1000 steps of service after t ~ 2000), checked on actions, rewards and
+    observations, then 20 external-action steps (k_env_ext) and the full state
+    (remaining runtimes exported from the finish keys) and counters, for 4 envs."""
+    from vmp.batched import BatchedVmEnv
+    cfg = dict(pms=100, vms=1000, arrival_rate=1.8182, service_length=1000,
+               training_steps=10000, eval_steps=100000, seed=0, reward_function="wr",
+               sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
+    N, CHK = 256, [0, 1, 97, 255]
+    seeds = 4 * np.arange(N, dtype=np.int64)
+    b = BatchedVmEnv(_cfg(cfg), N, seeds=seeds, device=DEV)
+    orc = {i: O.OracleEnv(dict(cfg, seed=int(seeds[i]))) for i in CHK}
+    for i, e in orc.items():
+        e.eval(False)
+        e.reset(int(seeds[i]))
+    FF = 2900
+    for k0 in range(0, FF, 100):
+        rs, _ = b.rollout("firstfit", 100)
+        rs = rs.cpu().numpy()
+        for k in range(100):
+            for i, e in orc.items():
+                _, r, _, _ = e.step(e.firstfit())
+                assert rs[k, i] == r, (k0 + k, i, rs[k, i], r)
+    served0 = b.counters().cpu().numpy()[:, 1].copy()
+    for t in range(200):
+        obs, rew, _, _, act = b.heuristic_step("firstfit", want_actions=True)
+        rew, act, obs = rew.cpu().numpy(), act.cpu().numpy(), obs.cpu().numpy()
+        for i, e in orc.items():
+            a = e.firstfit()
+            assert np.array_equal(a, act[i]), (t, i)
+            o, r, _, _ = e.step(a)
+            assert rew[i] == r, (t, i, rew[i], r)
+            assert np.array_equal(o, obs[i]), (t, i)
+    served1 = b.counters().cpu().numpy()[:, 1]
+    assert (served1 - served0).sum() > 10 * N, "no finishing VMs in the checked window"
+    for t in range(20):
+        acts = b.heuristic_act("firstfit")
+        obs, rew, _, _ = b.step(acts)
+        rew, obs = rew.cpu().numpy(), obs.cpu().numpy()
+        for i, e in orc.items():
+            o, r, _, _ = e.step(e.firstfit())
+            assert rew[i] == r and np.array_equal(o, obs[i]), (t, i)
+    sd = b.state()
+    ctr = b.counters().cpu().numpy()
+    for i, e in orc.items():
+        so = e.state()
+        for j, k in enumerate(("vm_placement", "vm_cpu", "vm_memory", "cpu", "memory",
+                               "vm_remaining_runtime")):
+            assert np.array_equal(sd[k][i].cpu().numpy(), so[j]), (k, i)
+        assert np.array_equal(ctr[i], e.counters()[0]), i
+    b.close()
