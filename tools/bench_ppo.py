@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--pms", type=int, default=100)
     ap.add_argument("--vms", type=int, default=300)
     ap.add_argument("--hidden", type=int, default=512)
-    ap.add_argument("--chunk-gb", type=float, default=4.0)
+    ap.add_argument("--chunk-gb", type=float, default=0.0, help="0: auto (1/8 of HBM)")
     ap.add_argument("--precision", default="f32", choices=["f32", "bf16"])
     args = ap.parse_args()
     from vmp.batched import BatchedVmEnv

@@ -66,7 +66,7 @@ class PPOConfig:
     # ---- build options (not in the reference) ----
     value_loss_broadcast: bool = True  # ppo.py:266-270 [mb,1]-[mb] broadcast
     precision: str = "f32"             # "bf16": bf16 GEMM inputs, f32 accumulate/output
-    chunk_bytes: int = 4 << 30         # logits budget per update chunk
+    chunk_bytes: int = 0               # logits budget per update chunk (0: 1/8 of HBM)
     seed_stride: int = 4               # env/episode reset seed spacing
 
 
@@ -608,7 +608,7 @@ class PPOTrainer:
                     ss = self._allreduce(((a_mb - mean) ** 2).sum().reshape(1).double())
                     std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
                     adv_n = (a_mb - mean) / (std + 1e-10)
-                ce = max(1, min(N, int(cfg.chunk_bytes) // max(1, mt * VA * 4)))
+                ce = max(1, min(N, self._chunk_bytes() // max(1, mt * VA * 4)))
                 self._zero_grads(params)
                 kl_sum = torch.zeros(1, dtype=torch.float64, device=rew.device)
                 clip_n = torch.zeros(1, dtype=torch.float64, device=rew.device)
@@ -667,6 +667,18 @@ class PPOTrainer:
             stats["clipfracs"] = torch.cat(clipfracs).double().cpu().tolist()
         self.stats = stats
         return stats
+
+    def _chunk_bytes(self):
+        """Logits budget per update chunk: PPOConfig.chunk_bytes, or 1/8 of the
+        device's memory (36 GB on a 288 GB MI355X: a whole config/100.yml
+        minibatch of 8192 envs, 25 GB of f32 logits, is one chunk, so backward
+        writes each gradient once instead of accumulating chunk by chunk)."""
+        if int(self.cfg.chunk_bytes) > 0:
+            return int(self.cfg.chunk_bytes)
+        dev = self.obs.device if getattr(self, "obs", None) is not None else None
+        if dev is None or dev.type != "cuda":
+            return 4 << 30
+        return int(torch.cuda.get_device_properties(dev).total_memory) // 8
 
     def _zero_grads(self, params):
         """Single process: grads re-created by backward. Data parallel: every
