@@ -2711,7 +2711,7 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
                                            BigShared &B, uint32_t LDSP *W,
                                            uint32_t (&rem)[SPT], uint32_t run0, uint32_t &dirty,
                                            int kstep, bool &terminated, float *out_obs,
-                                           bool store_state, int e STAMP_PARAMS) {
+                                           bool store_state, bool heur, int e STAMP_PARAMS) {
   const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
@@ -2733,13 +2733,21 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
   }
   dirty |= fterm;
   const int n_term = row_counts<SPT>(fterm, B);
+  // heuristic actions never suspend, so only the PMs freed here can fall under
+  // the precision clamp: they are clamped as they are freed (equal to the
+  // reference's clamp after all frees: once a PM's value is < 1e-7 every
+  // further free leaves it < 1e-7, and the clamp maps both to 0); external
+  // actions keep the full clamp pass below
+  const bool clamp_inline = heur;
 #pragma unroll 1
   for (int j0 = 0; j0 < n_term; j0 += 512) {
-    int base = 0;
+    if (ballot(fterm != 0)) {  // waves without finishers skip the ranking
+      int base = 0;
 VMP_SLOOP
-    for (int s = 0; s < SPT; s++) {
-      const int r = slot_rank(fterm, s, B, base);
-      if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) B.evw[r - j0] = W[s * NT + t];
+      for (int s = 0; s < SPT; s++) {
+        const int r = slot_rank(fterm, s, B, base);
+        if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) B.evw[r - j0] = W[s * NT + t];
+      }
     }
     __syncthreads();
     if (w0) {
@@ -2748,8 +2756,12 @@ VMP_SLOOP
       for (int i = 0; i < nt; i++) {  // frees in ascending VM order
         const uint32_t ew = B.evw[i];
         const int q = w_pl(ew);
-        const double cq = L.cpu[q] - T.cent[w_cc(ew)];
-        const double mq = L.mem[q] - T.cent[w_cm(ew)];
+        double cq = L.cpu[q] - T.cent[w_cc(ew)];
+        double mq = L.mem[q] - T.cent[w_cm(ew)];
+        if (clamp_inline) {
+          if (cq < 1e-7) cq = 0;
+          if (mq < 1e-7) mq = 0;
+        }
         wsync();
         if (lane == 0) {
           L.cpu[q] = cq;
@@ -2764,7 +2776,7 @@ VMP_SLOOP
   for (int s = 0; s < SPT; s++)
     if ((fterm >> s) & 1u) W[s * NT + t] = w_make(NUL, 0, 0);
   STAMP(2);
-  if (w0)
+  if (w0 && !clamp_inline)
     for (int i = lane; i < P; i += 64) {  // precision clamp
       if (L.cpu[i] < 1e-7) L.cpu[i] = 0;
       if (L.mem[i] < 1e-7) L.mem[i] = 0;
@@ -2799,6 +2811,7 @@ VMP_SLOOP
       int base = 0;
 #pragma unroll
       for (int s = 0; s < SPT; s++) {  // rem[] statically indexed
+        if (base >= j1) break;  // block-uniform: later rows rank past the accepted
         const int j = slot_rank(fnull, s, B, base);
         if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
           W[s * NT + t] = w_make(WAIT, L.accc[j], L.accm[j]);
@@ -2957,7 +2970,8 @@ VMP_SLOOP
     }
     __syncthreads();
     const double r = big_tail<SPT>(p, L, T, B, W, rem, run0, dirty, k, term,
-                                   last && o.obs ? o.obs + (int64_t)e * p.D : nullptr, last, e
+                                   last && o.obs ? o.obs + (int64_t)e * p.D : nullptr, last,
+                                   o.policy >= 0, e
                                    STAMP_ARGS);
     if (o.reward && t == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
