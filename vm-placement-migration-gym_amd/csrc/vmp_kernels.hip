@@ -2163,6 +2163,7 @@ struct BigShared {
   int32_t evt[512];   // event list: target / value
   uint8_t evok[512];  // event results
   double half[20];    // big_sum_phase: the two halves of a split job j at 2j, 2j + 1
+  uint32_t fmax[128]; // big_heuristic: the any-fit table of build_fitmax
 };
 
 // Rank of this thread's flag among the flagged threads of the block
@@ -2219,6 +2220,34 @@ __device__ __forceinline__ int slot_rank(uint32_t fl, int s, const BigShared &B,
   const int r = base + pre + below(m, lane);
   base += tot;
   return r;
+}
+
+// After row_counts: the block rank (VM order) of this wave's first flagged
+// slot of row s, in lane s (s < SPT), and in `rowbase` the rank of row s's
+// first flagged slot. One set of LDS reads per wave and a lane scan, instead
+// of eight LDS reads per row in slot_rank; then the rank of a flagged slot in
+// row s is readlane(result, s) + its position among the wave's flags.
+template <int SPT>
+__device__ __forceinline__ int row_prefix(const BigShared &B, int &rowbase) {
+  static_assert(SPT <= 32, "one lane per slot row");
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  int tot = 0, mine = 0;
+  if (lane < SPT) {
+#pragma unroll
+    for (int w = 0; w < kBigMaxWaves; w++) {  // rows of absent waves stay 0
+      const int c = B.rc[lane * kBigMaxWaves + w];
+      tot += c;
+      mine += w < wid ? c : 0;
+    }
+  }
+  int incl = tot;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  rowbase = incl - tot;
+  return rowbase + mine;
 }
 
 __device__ __forceinline__ int block_sum_int(int x, BigShared &B) {
@@ -2315,12 +2344,33 @@ VMP_SLOOP
       if (rebuild) {
         big_build_bitmaps(p, L);
         STAMP(22);
+        // which pending VMs fit some PM: the any-fit table (build_fitmax), one
+        // LDS read per pending VM instead of a scan of its two bitmap rows
+        uint32_t *M = B.fmax;
+        for (int i = t; i < 128; i += NT) M[i] = 0;  // NT may be 64
+        __syncthreads();
+        for (int q = t; q < P; q += NT) {
+          const int tcq = (int)L.tc[q];
+          if (tcq > 0) __atomic_fetch_max(&M[tcq - 1], (uint32_t)L.tm[q], __ATOMIC_RELAXED);
+        }
+        __syncthreads();
+        if (w0) {
+          const int rlo = 63 - lane, rhi = 127 - lane;
+          const bool hi_ok = rhi <= 100;
+          uint32_t c1 = hi_ok ? M[rhi] : 0u, c0 = M[rlo];
+          c1 = prefix_max32(c1);
+          c0 = max(prefix_max32(c0), (uint32_t)__builtin_amdgcn_readlane((int)c1, 63));
+          wsync();
+          M[rlo] = c0;
+          if (hi_ok) M[rhi] = c1;
+        }
+        __syncthreads();
         hit = 0;
 VMP_SLOOP
         for (int s = 0; s < SPT; s++)
           if ((pend >> s) & 1u) {
             const uint32_t w = W[s * NT + t];
-            if (bm_query(L, NW, w_cc(w), w_cm(w)) >= 0) hit |= 1u << s;
+            if (M[w_cc(w)] > (uint32_t)w_cm(w)) hit |= 1u << s;
           }
         rebuild = false;
         STAMP(17);
@@ -2742,10 +2792,11 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
 #pragma unroll 1
   for (int j0 = 0; j0 < n_term; j0 += 512) {
     if (ballot(fterm != 0)) {  // waves without finishers skip the ranking
-      int base = 0;
+      int rb;
+      const int pre = row_prefix<SPT>(B, rb);
 VMP_SLOOP
       for (int s = 0; s < SPT; s++) {
-        const int r = slot_rank(fterm, s, B, base);
+        const int r = __builtin_amdgcn_readlane(pre, s) + below(ballot((fterm >> s) & 1u), lane);
         if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) B.evw[r - j0] = W[s * NT + t];
       }
     }
@@ -2808,11 +2859,12 @@ VMP_SLOOP
         }
       }
       __syncthreads();
-      int base = 0;
+      int rb;
+      const int pre = row_prefix<SPT>(B, rb);
 #pragma unroll
       for (int s = 0; s < SPT; s++) {  // rem[] statically indexed
-        if (base >= j1) break;  // block-uniform: later rows rank past the accepted
-        const int j = slot_rank(fnull, s, B, base);
+        if (__builtin_amdgcn_readlane(rb, s) >= j1) break;  // later rows rank past the accepted
+        const int j = __builtin_amdgcn_readlane(pre, s) + below(ballot((fnull >> s) & 1u), lane);
         if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
           W[s * NT + t] = w_make(WAIT, L.accc[j], L.accm[j]);
           rem[s] = (uint32_t)B.evt[j - j0];
@@ -2843,10 +2895,11 @@ VMP_SLOOP
   n_w = block_sum_int(n_w, B);
   const int n_ex = row_counts<SPT>(fex, B);
   if (kl) {
-    int base = 0;
+    int rb;
+    const int pre = row_prefix<SPT>(B, rb);
 VMP_SLOOP
     for (int s = 0; s < SPT; s++) {
-      const int r = slot_rank(fex, s, B, base);
+      const int r = __builtin_amdgcn_readlane(pre, s) + below(ballot((fex >> s) & 1u), lane);
       if ((fex >> s) & 1u) {
         const uint32_t w = W[s * NT + t];
         L.ccomp[r] = (uint8_t)w_cc(w);
