@@ -397,3 +397,46 @@ def test_headline_steady_state_firstfit_vs_oracle():
             assert np.array_equal(sd[k][i].cpu().numpy(), so[j]), (k, i)
         assert np.array_equal(ctr[i], e.counters()[0]), i
     b.close()
+
+
+@pytest.mark.parametrize("big", [False, True], ids=["wave", "block"])
+def test_finish_keys_short_service_vs_oracle(big, monkeypatch):
+    """Finish keys under churn: service lengths of 1-6 steps
+    (Poisson(2) + 1), so VMs placed with one step left finish in the step that
+    places them, and external actions that suspend running VMs and re-place
+    waiting ones every step (WAIT <-> PM moves rewrite the time word by -t / +t).
+    The exported state — remaining runtimes included — and the counters must be
+    the oracle's after every step, through both env kernels."""
+    from vmp.batched import BatchedVmEnv
+    if big:
+        monkeypatch.setenv("VMP_BIG_KERNEL", "1")
+    base = dict(pms=12, vms=90, arrival_rate=3.0, service_length=2, training_steps=10000,
+                eval_steps=100000, allow_null_action=True, seed=0, reward_function="ut")
+    N, P = 6, 12
+    seeds = np.arange(N, dtype=np.int64) * 4 + 7
+    b = BatchedVmEnv(_cfg(base), N, seeds=seeds, device=DEV)
+    oes = [O.OracleEnv(dict(base, seed=int(s))) for s in seeds]
+    for e, s in zip(oes, seeds):
+        e.reset(int(s))
+    rng = np.random.default_rng(3)
+    keys = ("vm_placement", "vm_cpu", "vm_memory", "cpu", "memory", "vm_remaining_runtime")
+    for t in range(120):
+        pl = b.state()["vm_placement"].cpu().numpy()
+        acts = pl.copy()
+        u = rng.random(pl.shape)
+        susp = (pl < P) & (u < 0.2)
+        acts[susp] = P
+        wait = pl == P
+        acts[wait & (u < 0.7)] = rng.integers(0, P, size=pl.shape)[wait & (u < 0.7)]
+        _, rew, _, valid = b.step(torch.tensor(acts, dtype=torch.int32, device=DEV))
+        rew, valid = rew.cpu().numpy(), valid.cpu().numpy()
+        sd = {k: v.cpu().numpy() for k, v in b.state().items()}
+        ctr = b.counters().cpu().numpy()
+        for i, e in enumerate(oes):
+            _, r, _, v = e.step(acts[i])
+            assert rew[i] == r and np.array_equal(v, valid[i]), (t, i)
+            so = e.state()
+            for j, k in enumerate(keys):
+                assert np.array_equal(sd[k][i], so[j]), (t, i, k)
+            assert np.array_equal(ctr[i], e.counters()[0]), (t, i)
+    assert int(b.counters().cpu().numpy()[:, 2].sum()) > 100  # suspensions happened
