@@ -1268,43 +1268,24 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     }
     wsync();
     STAMP(16);
-    bool anyfit = false;
-    {  // the fit bitmaps are built only if some pending VM fits somewhere
+    // which pending VMs fit some PM, from the any-fit table; the fit bitmaps
+    // are built only if one does
+    uint32_t hit = 0;  // bit s: VM slot s of this lane is pending and some PM fits it
+    {
       uint32_t LDSP *M = reinterpret_cast<uint32_t LDSP *>(L.bc);
       build_fitmax(p, L, M);
 #pragma unroll
       for (int s = 0; s < VPT; s++)
-        anyfit |= ((pend >> s) & 1u) && M[w_cc(wa[s])] > (uint32_t)w_cm(wa[s]);
+        hit |= (uint32_t)(((pend >> s) & 1u) && M[w_cc(wa[s])] > (uint32_t)w_cm(wa[s])) << s;
     }
+    const bool anyfit = ballot(hit != 0) != 0;
     bool rebuild = true;
-    uint32_t hit = 0;  // bit s: VM slot s of this lane is pending and some PM fits it
 #pragma unroll 1
-    for (; ballot(anyfit);) {
+    for (; anyfit;) {
       if (rebuild) {  // single site: the initial build (index-order fit bitmaps)
         build_bitmaps(p, L, false);
         rebuild = false;
         STAMP(17);
-        // which pending VMs have any fit: branch-free row ANDs for P <= 128
-        // (every slot's rows are valid, pad slots read row 0), so the LDS
-        // reads of all slots are in flight together
-        hit = 0;
-        if (NW <= 2) {
-          const int nw = NW;
-#pragma unroll
-          for (int s = 0; s < VPT; s++) {
-            const uint64_t LDSP *rc = L.bc + w_cc(wa[s]) * nw;
-            const uint64_t LDSP *rm = L.bm + w_cm(wa[s]) * nw;
-            uint64_t a = rc[0] & rm[0];
-            if (nw == 2) a |= rc[1] & rm[1];
-            hit |= (uint32_t)(a != 0) << s;
-          }
-          hit &= pend;
-        } else {
-#pragma unroll
-          for (int s = 0; s < VPT; s++)
-            if (((pend >> s) & 1u) && bm_query(L, NW, w_cc(wa[s]), w_cm(wa[s])) >= 0)
-              hit |= 1u << s;
-        }
       }
       // earliest VM (index order) with a fit
       int ws = -1, wl = 0;
