@@ -608,7 +608,7 @@ class PPOTrainer:
                     ss = self._allreduce(((a_mb - mean) ** 2).sum().reshape(1).double())
                     std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
                     adv_n = (a_mb - mean) / (std + 1e-10)
-                ce = max(1, min(N, self._chunk_bytes() // max(1, mt * VA * 4)))
+                ce = max(1, min(N, self._chunk_bytes(rew.device) // max(1, mt * VA * 4)))
                 self._zero_grads(params)
                 kl_sum = torch.zeros(1, dtype=torch.float64, device=rew.device)
                 clip_n = torch.zeros(1, dtype=torch.float64, device=rew.device)
@@ -668,15 +668,14 @@ class PPOTrainer:
         self.stats = stats
         return stats
 
-    def _chunk_bytes(self):
+    def _chunk_bytes(self, dev):
         """Logits budget per update chunk: PPOConfig.chunk_bytes, or 1/8 of the
         device's memory (36 GB on a 288 GB MI355X: a whole config/100.yml
         minibatch of 8192 envs, 25 GB of f32 logits, is one chunk, so backward
         writes each gradient once instead of accumulating chunk by chunk)."""
         if int(self.cfg.chunk_bytes) > 0:
             return int(self.cfg.chunk_bytes)
-        dev = self.obs.device if getattr(self, "obs", None) is not None else None
-        if dev is None or dev.type != "cuda":
+        if dev.type != "cuda":
             return 4 << 30
         return int(torch.cuda.get_device_properties(dev).total_memory) // 8
 
