@@ -7,7 +7,13 @@ step for every env (the Base.test loop body, base.py:71-86) in training mode
 (info = {} as in env.py:168; the eval-mode info metrics are derived on demand
 by vmp_get_stats), obs/reward/done written to HBM each step. Envs per GPU fixed (weak scaling); env i of the job
 has seed 4*i. Before timing, every env is fast-forwarded to the
-steady-state fill (~200 running / ~800 waiting VMs) with the fused rollout.
+steady-state fill (~200 running / ~800 waiting VMs) with the fused rollout, with
+its phase staggered: the fill -> finish -> refill cycle of this workload
+repeats every ~L = 1000 steps (service ~ Poisson(1000) + 1), so the envs are
+reset in G = 10 groups 100 steps apart and are 2 600-3 500 steps old when the
+timed window starts, i.e. spread over one whole service period (a window in
+which every env sits in the same phase would time only that phase; the
+`period` leg times 1 000 consecutive launches of phase-aligned envs instead).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E]
        (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -63,6 +69,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=32768, help="envs per GPU")
     ap.add_argument("--ff-steps", type=int, default=2500, help="steady-state fast-forward")
+    ap.add_argument("--phase-groups", type=int, default=10,
+                    help="env groups reset --phase-delta steps apart before timing")
+    ap.add_argument("--phase-delta", type=int, default=100)
+    ap.add_argument("--period-steps", type=int, default=1000,
+                    help="period leg: consecutive launches of phase-aligned envs (0: skip)")
+    ap.add_argument("--period-ff", type=int, default=2000)
+    ap.add_argument("--period-only", action="store_true",
+                    help="run only the period leg (rocprofv3 of that window)")
+    ap.add_argument("--nominal-steps", type=int, default=50,
+                    help="C-main at nominal load (lambda 0.182) timed launches (0: skip)")
     ap.add_argument("--rollout-k", type=int, default=100, help="steps per fused rollout launch")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -107,13 +123,18 @@ def main():
     stream = torch.cuda.current_stream(dev)
     h = env._bind()
 
-    # ---- fast-forward to steady state (untimed) ----
-    ff = args.ff_steps
-    k = args.rollout_k
-    while ff > 0:
-        kk = min(k, ff)
-        env.rollout("firstfit", kk)
-        ff -= kk
+    if args.period_only:
+        env.close()
+        per = bench_period(args, dev, rank, world, dist, CFG)
+        if rank == 0:
+            print(json.dumps({"period": per}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    # ---- fast-forward to steady state, phases staggered (untimed) ----
+    reset_at, ff_total = fast_forward(env, "firstfit", seeds, args.ff_steps, args.phase_groups,
+                                      args.phase_delta, args.rollout_k)
     torch.cuda.synchronize(dev)
 
     obs = torch.empty((N, D), dtype=torch.float32, device=dev)
@@ -181,7 +202,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         r_el = float(t[0])
     fused_value = world * N * kr * nrep / r_el
-    steps_done = args.ff_steps + args.warmup + K + ext_steps + kr * (nrep + 1)
+    steps_done = ff_total + args.warmup + K + ext_steps + kr * (nrep + 1)
 
     # ---- replica reduction: counters summed, per-env returns of the
     # last fused rollout gathered over ranks (RCCL at N > 1) ----
@@ -209,14 +230,15 @@ def main():
             e = O.OracleEnv(dict(CFG, seed=int(seeds[i])))
             e.eval(False)
             e.reset(int(seeds[i]))
-            for s in range(steps_done - kr):
+            for s in range(steps_done - int(reset_at[i]) - kr):  # env i's age
                 e.step(e.firstfit())
             for s in range(kr):
                 _, r, _, _ = e.step(e.firstfit())
                 errs.append(abs(r - r_gpu[s, i]))
             ctr_ok &= bool(np.array_equal(e.counters()[0], ctr_gpu[i]))
         parity = {"reward_mae": float(np.mean(errs)), "counters_equal": ctr_ok,
-                  "envs_checked": n_chk, "steps_checked": steps_done}
+                  "envs_checked": n_chk,
+                  "steps_checked": [steps_done - int(reset_at[i]) for i in range(n_chk)]}
 
         if world == 1 and not args.no_cpu:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
@@ -239,6 +261,10 @@ def main():
         except Exception:
             traffic = None
     env.close()
+    period = None if args.period_steps <= 0 else _guard(bench_period, args, dev, rank, world,
+                                                       dist, CFG)
+    nominal = None if args.nominal_steps <= 0 else _guard(bench_nominal, args, dev, rank, world,
+                                                         dist)
     ppo_train = ppo_train_bf16 = ppo_eval = None
     if not args.no_ppo:
         ppo_train = _guard(bench_ppo_train, args, dev, rank, world, dist)
@@ -254,7 +280,10 @@ def main():
                    "global_envs": world * N, "pms": P, "vms": V,
                    "arrival_rate": CFG["arrival_rate"], "service_length": CFG["service_length"],
                    "reward_function": "wr", "policy": "firstfit", "mode": "train",
-                   "parallelism": f"env-shard x{world}", "steady_state_ff_steps": args.ff_steps},
+                   "parallelism": f"env-shard x{world}", "steady_state_ff_steps": args.ff_steps,
+                   "phase_stagger": f"{args.phase_groups} groups x {args.phase_delta} steps: "
+                                    f"env ages {ff_total - (args.phase_groups - 1) * args.phase_delta}"
+                                    f"-{ff_total} at the window"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "vmp::k_env<16, true> (heuristic act+step, one step per launch)", "kernel_ms": kern_ms,
@@ -262,6 +291,8 @@ def main():
         "cpu_baseline": cpu,
         "reference_cpu": _reference_cpu(),
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},
+        "period": period,
+        "nominal_load": nominal,
         "external_actions": ext,
         "replicas": replicas,
         "parity": parity,
@@ -274,6 +305,165 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def fast_forward(env, policy, seeds, ff, groups, delta, k):
+    """Fused-rollout fast-forward with staggered phases: env i (group i mod
+    `groups`) is reset with its own seed at step (i mod groups) * delta, so after
+    ff + (groups - 1) * delta steps the envs' ages are spread over
+    (groups - 1) * delta steps. Returns (reset step per env, total steps)."""
+    N = env.n_envs
+    groups = max(1, int(groups))
+    grp = np.arange(N) % groups
+    reset_at = grp * delta
+    total = ff + (groups - 1) * delta
+    events = [g * delta for g in range(1, groups)]
+    t = 0
+    while t < total:
+        if t in events:
+            env.reset(seeds, mask=torch.from_numpy(grp == t // delta), obs=False)
+        nxt = min([x for x in events if x > t] + [total])
+        kk = min(k, nxt - t)
+        env.rollout(policy, kk)
+        t += kk
+    return reset_at, total
+
+
+def bench_period(args, dev, rank, world, dist, cfg):
+    """the headline workload over a whole service period.
+    Phase-aligned envs (all reset together, as at the start of an episode)
+    fast-forwarded --period-ff = 2 000 steps, then --period-steps = 1 000
+    consecutive per-step launches (steps 2 001-3 000: the refill burst after
+    the first VMs finish, and the quiet phase after it). Per-launch kernel
+    time from a HIP event pair around every launch on the launch stream;
+    mean / max and 100-launch bins, changed VM words and the roofline of the
+    window's mean launch."""
+    from vmp import _lib
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.replicas import shard_seeds
+    N = args.envs
+    P, V = cfg["pms"], cfg["vms"]
+    env = BatchedVmEnv(Config(**cfg), N, seeds=shard_seeds(rank, N), device=dev)
+    env.eval(False)
+    left = args.period_ff
+    while left > 0:
+        env.rollout("firstfit", min(args.rollout_k, left))
+        left -= args.rollout_k
+    L, h = _lib.lib(), env._bind()
+    stream = torch.cuda.current_stream(dev)
+    obs = torch.empty((N, 3 * V + 2 * P), dtype=torch.float32, device=dev)
+    rew = torch.empty((N,), dtype=torch.float64, device=dev)
+    done = torch.empty((N,), dtype=torch.uint8, device=dev)
+    p_obs, p_rew, p_done = _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done)
+    K = args.period_steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    c0 = env.counters()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        _lib.check(L.vmp_heuristic_step(h, 0, None, p_obs, p_rew, p_done, None))
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    c1 = env.counters()
+    words = changed_words(c0, c1, N * K)
+    ms = np.array([a.elapsed_time(b) for a, b in ev])
+    env.close()
+    mean_ms = _max_over_ranks(float(ms.mean()), dev, dist)
+    bins = [round(float(ms[i:i + 100].mean()), 4) for i in range(0, K, 100)]
+    bpe = step_bytes(P, V, words)
+    ach = bpe * N / (mean_ms * 1e-3) / 1e9
+    return {"value": world * N / (mean_ms * 1e-3), "unit": "env-steps/s",
+            "value_kind": "mean per-launch kernel time over the window",
+            "wall_value": world * N * K / el,
+            "window": f"steps {args.period_ff + 1}-{args.period_ff + K} of phase-aligned envs",
+            "steps": K, "mean_ms": mean_ms, "max_ms": float(ms.max()),
+            "min_ms": float(ms.min()), "ms_by_100_steps": bins,
+            "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS,
+                         "kernel": "vmp::k_env<16, true> (heuristic act+step)"}}
+
+
+def bench_nominal(args, dev, rank, world, dist):
+    """SURVEY §8(d) C-main at nominal load: config/100.yml with vms = 1000 at
+    lambda = 0.182 (100 % load, exp_suspension.py:19; ~724 NULL slots and ~121
+    waiting VMs per env), L = 1000, reward wr, FirstFit act + step per launch,
+    phases staggered as the headline's; its own roofline (same byte model) and
+    its own CPU baseline (the C oracle, OpenMP, rank 0 at N = 1)."""
+    from vmp import _lib
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.replicas import shard_seeds
+    cfg = dict(CFG, arrival_rate=0.182)
+    N = args.envs
+    P, V = cfg["pms"], cfg["vms"]
+    seeds = shard_seeds(rank, N)
+    env = BatchedVmEnv(Config(**cfg), N, seeds=seeds, device=dev)
+    env.eval(False)
+    _, ff_total = fast_forward(env, "firstfit", seeds, 2000, args.phase_groups, args.phase_delta,
+                               args.rollout_k)
+    L, h = _lib.lib(), env._bind()
+    stream = torch.cuda.current_stream(dev)
+    obs = torch.empty((N, 3 * V + 2 * P), dtype=torch.float32, device=dev)
+    rew = torch.empty((N,), dtype=torch.float64, device=dev)
+    done = torch.empty((N,), dtype=torch.uint8, device=dev)
+    p_obs, p_rew, p_done = _lib.ptr(obs), _lib.ptr(rew), _lib.ptr(done)
+    for _ in range(5):
+        _lib.check(L.vmp_heuristic_step(h, 0, None, p_obs, p_rew, p_done, None))
+    pl = env.state()["vm_placement"]
+    running = float((pl < P).sum(1).double().mean())
+    waiting = float((pl == P).sum(1).double().mean())
+    del pl
+    K = args.nominal_steps
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    c0 = env.counters()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(K):
+        _lib.check(L.vmp_heuristic_step(h, 0, None, p_obs, p_rew, p_done, None))
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    words = changed_words(c0, env.counters(), N * K)
+    kern_ms = _max_over_ranks(ev0.elapsed_time(ev1) / K, dev, dist)
+    env.close()
+    bpe = step_bytes(P, V, words)
+    ach = bpe * N / (kern_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import oracle as O
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        n_cpu, warm_cpu, steps_cpu = 4 * threads, 2000, 4000
+        sec, _ = O.rollout_timed(cfg, n_cpu, 0, 4, warm_cpu, steps_cpu, 0, threads)
+        cpu = {"value": n_cpu * steps_cpu / sec, "unit": "env-steps/s", "cores": threads,
+               "kind": "port",
+               "sample": f"{n_cpu} envs x {steps_cpu} FirstFit act+step after {warm_cpu} "
+                         f"warm-up steps, OpenMP {threads} threads (C oracle, lambda 0.182)"}
+    return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
+            "workload": "config/100.yml with vms=1000, lambda 0.182 (100 % load), L 1000, "
+                        "reward wr, FirstFit act + step, one launch per step",
+            "envs_per_gpu": N, "ff_steps": ff_total, "steps": K, "mean_running": running,
+            "mean_waiting": waiting, "ms_per_step": 1e3 * el / K, "kernel_ms": kern_ms,
+            "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS,
+                         "kernel": "vmp::k_env<16, true> (heuristic act+step)"},
+            "cpu_baseline": cpu}
 
 
 def _guard(fn, *a):

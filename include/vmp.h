@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 6
+#define VMP_ABI_VERSION 7
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -153,6 +153,13 @@ int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward,
  * on the current observation of every env -> device int32[n_env][V]. */
 int vmp_heuristic_act(vmp_handle *h, int32_t policy, int32_t *actions);
 
+/* The same agents on a CALLER's observation, device f32[n_env][3V+2P]
+ * (firstfit.py:21-38 / bestfit.py:21-40 read only the obs they are passed,
+ * utils.py:37-47): f32 fit tests on the obs values, FirstFit updating cpu
+ * only, BestFit in flip(argsort(cpu+memory)) order with numpy's scalar
+ * introsort ties; no env state is read. -> device int32[n_env][V]. P <= 3583. */
+int vmp_heuristic_act_obs(vmp_handle *h, int32_t policy, const float *obs, int32_t *actions);
+
 /* act + step fused in one launch: the action the heuristic takes on the
  * pre-step observation is applied by step() in the same kernel (the
  * Base.test loop body, base.py:71-86). actions_out (nullable) receives it. */
@@ -263,6 +270,12 @@ int vmp_record_enable(vmp_handle *h, int32_t on);
  * over every VM life incl. the open ones; sums f64[n_env][VMP_NREC]. The
  * Record.get_summary values follow from these (vmp/record.py). */
 int vmp_record_read(vmp_handle *h, uint32_t *hist, double *sums);
+
+/* Fault injection (tests only): the n-th device allocation made by the
+ * library from now on fails as out of memory (n = 0: off). Drives the
+ * failure and cleanup paths of vmp_create / vmp_record_enable / vmp_mask_bool
+ * under the host sanitizers (tests/native/capi_faults.cpp). */
+int vmp_debug_fail_alloc(int32_t n);
 
 /* Diagnostics: per-env shader-clock cycles per kernel phase, accumulated since
  * the previous call, device u64[n_env][24] (see tools/stamps.py for the phase names).

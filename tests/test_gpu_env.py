@@ -341,17 +341,20 @@ def test_c5_steady_state_bestfit_kl_vs_oracle():
     b.close()
 
 
-def test_headline_steady_state_firstfit_vs_oracle():
+@pytest.mark.parametrize("lam, FF", [(1.8182, 2900), (0.182, 2000)])
+def test_headline_steady_state_firstfit_vs_oracle(lam, FF):
     """The bench workload (BASELINE headline: config/100.yml with vms = 1000,
-    L = 1000, reward wr, FirstFit, training mode) at its steady state: 256 envs
-    (seeds 4·i as bench.py's) fast-forwarded 2900 steps by the fused rollout,
-    whose rewards must equal the oracle's, then 200 per-step act+step launches
-    (k_env<16, true>) through the VMs placed in the refill burst finishing
-    (~1000 steps of service after t ~ 2000), checked on actions, rewards and
-    observations, then 20 external-action steps (k_env_ext) and the full state
-    (remaining runtimes exported from the finish keys) and counters, for 4 envs."""
+    L = 1000, reward wr, FirstFit, training mode) at its steady state, at the
+    shipped lambda = 1.8182 (10x load, ~800 waiting VMs) and at SURVEY §8(d)
+    C-main's nominal lambda = 0.182 (100 % load, exp_suspension.py:19: ~724
+    NULL slots, ~121 waiting): 256 envs (seeds 4·i as bench.py's)
+    fast-forwarded FF >= 2·L steps by the fused rollout, whose rewards must
+    equal the oracle's, then 200 per-step act+step launches (k_env<16, true>)
+    with VMs finishing, checked on actions, rewards and observations, then 20
+    external-action steps (k_env_ext) and the full state (remaining runtimes
+    exported from the finish keys) and counters, for 4 envs."""
     from vmp.batched import BatchedVmEnv
-    cfg = dict(pms=100, vms=1000, arrival_rate=1.8182, service_length=1000,
+    cfg = dict(pms=100, vms=1000, arrival_rate=lam, service_length=1000,
                training_steps=10000, eval_steps=100000, seed=0, reward_function="wr",
                sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
     N, CHK = 256, [0, 1, 97, 255]
@@ -361,7 +364,6 @@ def test_headline_steady_state_firstfit_vs_oracle():
     for i, e in orc.items():
         e.eval(False)
         e.reset(int(seeds[i]))
-    FF = 2900
     for k0 in range(0, FF, 100):
         rs, _ = b.rollout("firstfit", 100)
         rs = rs.cpu().numpy()
@@ -440,3 +442,32 @@ def test_finish_keys_short_service_vs_oracle(big, monkeypatch):
                 assert np.array_equal(sd[k][i], so[j]), (t, i, k)
             assert np.array_equal(ctr[i], e.counters()[0]), (t, i)
     assert int(b.counters().cpu().numpy()[:, 2].sum()) > 100  # suspensions happened
+
+
+def test_nominal_load_extra_null_slots_do_not_change_the_trajectory():
+    """at lambda = 0.182 (100 % load) free slots never run out, so
+    V = 300 (config/100.yml) and V = 1000 (the headline's vms) must walk the
+    same trajectory: equal rewards at every one of 2 500 fused FirstFit steps,
+    equal counters, no drops, equal PM loads. A size-independent check of the
+    full-size C-main nominal workload (64 envs per V)."""
+    from vmp.batched import BatchedVmEnv
+    N = 64
+    base = dict(pms=100, arrival_rate=0.182, service_length=1000, training_steps=10000,
+                eval_steps=100000, seed=0, reward_function="wr", sequence="uniform",
+                cap_target_util=True, beta=0.5, allow_null_action=True)
+    seeds = 4 * np.arange(N, dtype=np.int64)
+    envs = {V: BatchedVmEnv(_cfg(dict(base, vms=V)), N, seeds=seeds, device=DEV)
+            for V in (300, 1000)}
+    for k in range(5):
+        r = {V: e.rollout("firstfit", 500)[0].cpu().numpy() for V, e in envs.items()}
+        assert np.array_equal(r[300], r[1000]), k
+    c = {V: e.counters().cpu().numpy() for V, e in envs.items()}
+    assert np.array_equal(c[300], c[1000])
+    assert c[300][:, 4].sum() == 0, "drops: the invariance does not apply"
+    st = {V: e.state() for V, e in envs.items()}
+    for k in ("cpu", "memory"):
+        assert torch.equal(st[300][k], st[1000][k]), k
+    pl3, pl10 = st[300]["vm_placement"].cpu(), st[1000]["vm_placement"].cpu()
+    assert torch.equal(pl3, pl10[:, :300]) and bool((pl10[:, 300:] == 101).all())
+    for e in envs.values():
+        e.close()

@@ -9,7 +9,9 @@ reward wr), src/agents/ppo.py:172-295.
     through the C oracle are bit-exact on masks, observations, f64->f32
     rewards and counters (App. C item 4); every sampled action is valid under
     its mask; the update equals the same trainer with the plain-PyTorch
-    reference head and GAE (tests/torch_ref.py) within 1e-5 relative."""
+    reference head and GAE (tests/torch_ref.py) within 3e-4 relative L2 of
+    the parameter change (measured 1.2e-4: f32 summation order of the
+    300-term logprob sums and of the 30 600-wide head, 4 epochs deep)."""
 import os
 
 import numpy as np
@@ -38,17 +40,21 @@ def _need_gpu():
 def test_update_matches_reference_100yml_on_gpu(k_epochs):
     """PPOAgent.update (ppo.py:229-295) at the 100.yml shape through the HIP head
     and GAE against the reference's (tests/test_ppo_cpu.py ppo100_check: 2
-    epochs within 2e-6; 4 epochs the same minibatch / KL-break sequence and 5 %
-    of the update)."""
-    from tests.test_ppo_cpu import _ppo100_update, ppo100_check
+    epochs within 2e-6; 4 epochs the same minibatch / KL-break sequence, every
+    AdamW step before the first clip-branch flip within 5e-5 relative
+    (ppo100_step_check), and 5 % of the update at the end)."""
+    from tests.test_ppo_cpu import _ppo100_update, ppo100_check, ppo100_step_check
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
     from vmp.ppo import PPOAgent, PPOConfig
     env = BatchedVmEnv(Config(**CFG100), 1, device=DEV)
     ag = PPOAgent(env, PPOConfig(hidden_size=8, episodes=1, batch_size=100, minibatch_size=25,
                                  migration_ratio=0.002, k_epochs=k_epochs))
-    d, ag, st = _ppo100_update(k_epochs, agent=ag)
+    trace = {} if k_epochs == 4 else None
+    d, ag, st = _ppo100_update(k_epochs, agent=ag, trace=trace)
     ppo100_check(d, ag.model, st, k_epochs, atol_e2=2e-6)
+    if trace is not None:  # step by step up to the first clip-branch flip
+        assert ppo100_step_check(trace) >= 4
     env.close()
 
 
@@ -112,8 +118,7 @@ def test_trainer_100yml_replay_validity_and_reference_update():
     rel = (num / den) ** 0.5
     print(f"config-3 update: HIP vs torch-reference head, relative L2 of the parameter change "
           f"{rel:.2e}, max |diff| / max |change| {worst:.2e}")
-    # identical but for f32 summation order of 300-term logprob sums (see
-    # tests/test_ppo_cpu.py ppo100_check): 1e-5 relative unless a sample's
-    # clip branch flips (none at this seed)
-    assert rel < 1e-3, rel  # measured 1.2e-4
+    # identical but for the f32 summation order of 300-term logprob sums
+    # (see tests/test_ppo_cpu.py ppo100_check), compounded over 16 AdamW steps
+    assert rel < 3e-4, rel  # measured 1.2e-4
     env.close()

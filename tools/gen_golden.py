@@ -384,10 +384,73 @@ def gen_ppo100():
           max(float(np.abs(after[k] - before[k]).max()) for k in before))
 
 
+def gen_ppo100_steps():
+    """Per-step trace of the reference's 4-epoch update at the config/100.yml
+    shape (same model, batch and seeds as gen_ppo100, whose fixture it reads):
+    after every AdamW step, the flat parameter vector (state_dict keys sorted)
+    at 8192 fixed random positions; for every minibatch the reference
+    evaluates, its new log-probabilities and new values (ppo.py:258, 266),
+    from which the test finds the first minibatch whose clip branches differ
+    (ppo.py:267-280). Pins the update step by step where the final-parameter
+    check (5 % after a clip-branch flip) cannot."""
+    from src.agents.ppo import PPOAgent, PPOConfig
+    d = np.load(os.path.join(OUT, "ppo100_update.npz"))
+    B, V, A, D = (int(x) for x in d["shape"])
+    torch.manual_seed(0)
+    np.random.seed(0)
+    c = dict(BASE, pms=100, vms=300, service_length=1000, arrival_rate=1.8182,
+             training_steps=10000, eval_steps=100000, seed=0, reward_function="wr",
+             cap_target_util=True, allow_null_action=True)
+    env = make_env(c, "wr")
+    agent = PPOAgent(env, PPOConfig(hidden_size=8, episodes=1, batch_size=100,
+                                    minibatch_size=25, migration_ratio=0.002, k_epochs=4,
+                                    training_progress_bar=False))
+    model = agent.model
+    model.load_state_dict({k[3:]: torch.tensor(d[k]) for k in d.files if k.startswith("p0_")})
+    agent.optimizer = torch.optim.AdamW(model.parameters(), lr=agent.config.lr)
+    keys = sorted(model.state_dict())
+    n = sum(model.state_dict()[k].numel() for k in keys)
+    idx = np.sort(np.random.default_rng(20261017).choice(n, 8192, replace=False))
+
+    def flat():
+        sd = model.state_dict()
+        return torch.cat([sd[k].detach().flatten() for k in keys]).numpy()[idx].copy()
+    trace = {"p": [flat()], "lp": [], "v": []}
+    ga, gv, st = model.get_action, model.get_value, agent.optimizer.step
+
+    def get_action(*a, **k):
+        out = ga(*a, **k)
+        trace["lp"].append(out[1].detach().numpy().copy())
+        return out
+
+    def get_value(*a, **k):
+        out = gv(*a, **k)
+        trace["v"].append(out.detach().numpy().reshape(-1).copy())
+        return out
+
+    def step(*a, **k):
+        r = st(*a, **k)
+        trace["p"].append(flat())
+        return r
+    model.get_action, model.get_value, agent.optimizer.step = get_action, get_value, step
+    mask = np.unpackbits(d["b_mask_bits"], axis=1)[:, :V * A].reshape(B, V, A).astype(bool)
+    agent.update(torch.tensor(mask), torch.tensor(d["b_action"].astype(np.int64)),
+                 *[torch.tensor(d[k]) for k in ("b_obs", "b_next_obs", "b_logprob",
+                                                "b_reward", "b_done")])
+    # the two leading get_value calls are values / next_values (ppo.py:235-236)
+    out = {"idx": idx.astype(np.int64), "p": np.stack(trace["p"]),
+           "lp": np.stack(trace["lp"]), "v": np.stack(trace["v"][2:]),
+           "values": trace["v"][0], "next_values": trace["v"][1]}
+    np.savez_compressed(os.path.join(OUT, "ppo100_steps.npz"), **out)
+    print("ppo100 steps done:", out["p"].shape, out["lp"].shape, out["v"].shape)
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["rng", "traj", "ppo", "ppo100"]
     if "ppo100" in what:
         gen_ppo100()
+    if "ppo100" in what or "ppo100_steps" in what:
+        gen_ppo100_steps()
     if "rng" in what:
         gen_rng_kat()
     if "traj" in what:

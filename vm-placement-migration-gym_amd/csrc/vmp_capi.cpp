@@ -4,6 +4,8 @@
 // carve-out, and kernel dispatch on the handle's stream.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -36,6 +38,7 @@ __global__ void k_record(EnvParams p, RecArgs r);
 __global__ void k_record_init(EnvParams p, RecArgs r);
 __global__ void k_record_close(EnvParams p, RecArgs r, uint32_t *hist, double *sums);
 __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, uint8_t *mask);
+__global__ void k_act_obs(int P, int V, int policy, const float *obs, int32_t *act);
 }  // namespace vmp
 
 using namespace vmp;
@@ -55,6 +58,22 @@ int fail(int code, const std::string &msg) {
       return fail(_e == hipErrorOutOfMemory ? VMP_EOOM : VMP_EDEVICE,              \
                   std::string(#expr) + ": " + hipGetErrorString(_e));              \
   } while (0)
+
+// Device allocations of the handle go through here, so the failure paths can
+// be exercised (vmp_debug_fail_alloc: the n-th allocation from now fails as
+// out-of-memory; tests/test_sanitizers_cpu.py, tests/native/capi_faults.cpp).
+std::atomic<int64_t> g_fail_alloc{0};
+template <class T>
+hipError_t dev_malloc(T **p, size_t bytes) {
+  int64_t n = g_fail_alloc.load();
+  while (n > 0 && !g_fail_alloc.compare_exchange_weak(n, n - 1)) {
+  }
+  if (n == 1) {
+    *p = nullptr;
+    return hipErrorOutOfMemory;
+  }
+  return hipMalloc(reinterpret_cast<void **>(p), bytes);
+}
 
 // random_loggam (numpy distributions.c), host copy for the PTRS table.
 double loggam_host(double x) {
@@ -137,7 +156,7 @@ int setup_pois(double lam, PoisConst &c, double **dev_tab, std::vector<double> &
     host_tab.resize((size_t)n);
     for (int64_t k = 0; k < n; k++) host_tab[(size_t)k] = loggam_host((double)k);
     c.tab_n = (int32_t)n;
-    HIP_TRY(hipMalloc(dev_tab, sizeof(double) * n));
+    HIP_TRY(dev_malloc(dev_tab, sizeof(double) * n));
     HIP_TRY(hipMemcpy(*dev_tab, host_tab.data(), sizeof(double) * n, hipMemcpyHostToDevice));
     c.loggam_tab = *dev_tab;
   }
@@ -340,9 +359,9 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
 // vmp_create after the handle exists: every failure returns a code and the
 // caller destroys the handle (vmp_destroy tolerates what was not allocated).
 static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, const int64_t *seeds) {
-  hipError_t e1 = hipMalloc(&h->vmw, sizeof(uint64_t) * (size_t)n_env * h->V);
-  hipError_t e2 = hipMalloc(&h->pm, sizeof(double) * (size_t)n_env * 2 * h->P);
-  hipError_t e3 = hipMalloc(&h->hdr, sizeof(EnvHdr) * (size_t)n_env);
+  hipError_t e1 = dev_malloc(&h->vmw, sizeof(uint64_t) * (size_t)n_env * h->V);
+  hipError_t e2 = dev_malloc(&h->pm, sizeof(double) * (size_t)n_env * 2 * h->P);
+  hipError_t e3 = dev_malloc(&h->hdr, sizeof(EnvHdr) * (size_t)n_env);
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
     return fail(VMP_EOOM, "device allocation failed");
   HIP_TRY(hipMemset(h->hdr, 0, sizeof(EnvHdr) * (size_t)n_env));
@@ -363,7 +382,7 @@ static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, cons
   p.seq_range = hi - p.seq_lo;  // Generator.uniform: low + (high-low)*u
   {
     PoisConst pc[2] = {h->arr, h->svc};
-    HIP_TRY(hipMalloc(&h->pois_dev, sizeof(pc)));
+    HIP_TRY(dev_malloc(&h->pois_dev, sizeof(pc)));
     HIP_TRY(hipMemcpy(h->pois_dev, pc, sizeof(pc), hipMemcpyHostToDevice));
     p.pois = h->pois_dev;
     // PCG64 jump table for the lane-parallel draws (k_env prologue)
@@ -378,7 +397,7 @@ static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, cons
       A *= a;
       M = M * a + 1;
     }
-    HIP_TRY(hipMalloc(&h->jump_dev, sizeof(jt)));
+    HIP_TRY(dev_malloc(&h->jump_dev, sizeof(jt)));
     HIP_TRY(hipMemcpy(h->jump_dev, jt, sizeof(jt), hipMemcpyHostToDevice));
     p.jump = h->jump_dev;
   }
@@ -387,7 +406,7 @@ static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, cons
   p.hdr = h->hdr;
   carve(h);
 #ifdef VMP_STAMPS
-  HIP_TRY(hipMalloc(&h->stamps, sizeof(uint64_t) * kStamps * (size_t)n_env));
+  HIP_TRY(dev_malloc(&h->stamps, sizeof(uint64_t) * kStamps * (size_t)n_env));
   HIP_TRY(hipMemset(h->stamps, 0, sizeof(uint64_t) * kStamps * (size_t)n_env));
   p.stamps = h->stamps;
 #endif
@@ -407,7 +426,7 @@ static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, cons
   }
   refresh_params(h);
   int64_t *dseeds = nullptr;
-  HIP_TRY(hipMalloc(&dseeds, sizeof(int64_t) * n_env));
+  HIP_TRY(dev_malloc(&dseeds, sizeof(int64_t) * n_env));
   hipError_t e = hipMemcpy(dseeds, seeds, sizeof(int64_t) * n_env, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
     dim3 grid((n_env + kWavesPerBlock - 1) / kWavesPerBlock), block(64 * kWavesPerBlock);
@@ -498,6 +517,18 @@ int vmp_heuristic_act(vmp_handle *h, int32_t policy, int32_t *actions) {
   o.act_out = actions;
   o.k_steps = 0;
   return launch_env(h, o);
+}
+
+int vmp_heuristic_act_obs(vmp_handle *h, int32_t policy, const float *obs, int32_t *actions) {
+  if (!h || !obs || !actions) return fail(VMP_EINVAL, "null handle, obs or actions");
+  if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
+    return fail(VMP_EINVAL, "unknown policy");
+  const size_t lds = 18 * (size_t)h->P + 1024;  // cpu, memory, keys, order, sort stack
+  if (lds > 65536) return fail(VMP_EINVAL, "act from observation supports P <= 3583");
+  hipLaunchKernelGGL(k_act_obs, dim3(h->N), dim3(64), lds, h->stream, h->P, h->V, policy, obs,
+                     actions);
+  HIP_TRY(hipGetLastError());
+  return VMP_OK;
 }
 
 static int heuristic_step_impl(vmp_handle *h, int32_t policy, int32_t *actions_out, float *obs,
@@ -591,15 +622,24 @@ int vmp_record_enable(vmp_handle *h, int32_t on) {
   }
   const size_t nv = (size_t)h->N * h->V;
   if (!h->rec.prev) {
-    HIP_TRY(hipMalloc(&h->rec.prev, sizeof(uint16_t) * nv));
-    HIP_TRY(hipMalloc(&h->rec.life_n, sizeof(uint32_t) * nv));
-    HIP_TRY(hipMalloc(&h->rec.alloc, sizeof(int32_t) * nv));
-    HIP_TRY(hipMalloc(&h->rec.waits, sizeof(uint32_t) * nv));
-    HIP_TRY(hipMalloc(&h->rec.hist, sizeof(uint32_t) * (size_t)h->N * 2 * VMP_REC_BINS));
-    HIP_TRY(hipMalloc(&h->rec.sums, sizeof(double) * (size_t)h->N * VMP_NREC));
-    HIP_TRY(hipMalloc(&h->rec_act, sizeof(int32_t) * nv));
-    HIP_TRY(hipMalloc(&h->rec_valid, nv));
-    HIP_TRY(hipMalloc(&h->rec_reward, sizeof(double) * (size_t)h->N));
+    // all or nothing: a partial set would leave null buffers behind a
+    // non-null `prev` for the next call's k_record_init to write through
+    const hipError_t e[9] = {
+        dev_malloc(&h->rec.prev, sizeof(uint16_t) * nv),
+        dev_malloc(&h->rec.life_n, sizeof(uint32_t) * nv),
+        dev_malloc(&h->rec.alloc, sizeof(int32_t) * nv),
+        dev_malloc(&h->rec.waits, sizeof(uint32_t) * nv),
+        dev_malloc(&h->rec.hist, sizeof(uint32_t) * (size_t)h->N * 2 * VMP_REC_BINS),
+        dev_malloc(&h->rec.sums, sizeof(double) * (size_t)h->N * VMP_NREC),
+        dev_malloc(&h->rec_act, sizeof(int32_t) * nv),
+        dev_malloc(&h->rec_valid, nv),
+        dev_malloc(&h->rec_reward, sizeof(double) * (size_t)h->N)};
+    for (hipError_t x : e)
+      if (x != hipSuccess) {
+        vmp_record_enable(h, 0);
+        return fail(x == hipErrorOutOfMemory ? VMP_EOOM : VMP_EDEVICE,
+                    std::string("vmp_record_enable: ") + hipGetErrorString(x));
+      }
   }
   size_t n = nv;
   if ((size_t)h->N * 2 * VMP_REC_BINS > n) n = (size_t)h->N * 2 * VMP_REC_BINS;
@@ -634,7 +674,7 @@ int vmp_mask(vmp_handle *h, uint32_t *bits) {
 int vmp_mask_bool(vmp_handle *h, uint8_t *mask) {
   if (!h || !mask) return fail(VMP_EINVAL, "null argument");
   if (!h->scratch_bits)
-    HIP_TRY(hipMalloc(&h->scratch_bits, sizeof(uint32_t) * (size_t)h->N * h->V * h->W32));
+    HIP_TRY(dev_malloc(&h->scratch_bits, sizeof(uint32_t) * (size_t)h->N * h->V * h->W32));
   int rc = vmp_mask(h, h->scratch_bits);
   if (rc) return rc;
   int64_t rows = (int64_t)h->N * h->V;
@@ -689,6 +729,12 @@ int vmp_get_rank(vmp_handle *h, int64_t *rank) {
   hipLaunchKernelGGL(k_rank, dim3(h->N), dim3(64), sizeof(uint64_t) * ((h->P + 63) / 64),
                      h->stream, h->prm, rank);
   HIP_TRY(hipGetLastError());
+  return VMP_OK;
+}
+
+int vmp_debug_fail_alloc(int32_t n) {
+  if (n < 0) return fail(VMP_EINVAL, "n must be >= 0");
+  g_fail_alloc.store(n);
   return VMP_OK;
 }
 

@@ -3128,4 +3128,124 @@ __global__ __launch_bounds__(64) void k_target_means_lds(EnvParams p) {
   }
 }
 
+// ---- FirstFitAgent.act / BestFitAgent.act on a caller's observation --------
+// firstfit.py:21-38 / bestfit.py:21-40 exactly as written: the agent reads
+// only the f32 observation it is passed (convert_obs_to_dict, utils.py:37-47),
+// so this kernel takes obs f32[n_env][3V + 2P] and nothing of the env state.
+// The obs need not be one the env produced (an edited or stale observation):
+// fits are the f32 sums cpu[p] + vm_cpu[v] <= 1 and memory[p] + vm_memory[v]
+// <= 1, FirstFit updates only cpu[p], BestFit both, and BestFit visits the PMs
+// in flip(argsort(cpu + memory)) with numpy's scalar introsort tie order
+// (wave_aquicksort). One wave per env; the waiting VMs are
+// taken in index order, one PM scan (P/64 compares per lane) each. LDS:
+// cpu, memory, keys f32[P], order u16[P], sort stack i32[256] + scratch
+// u16[2P]. Not the hot path (the Base.test loop and the bench act on the
+// env's own state, k_env); this is the contract of act(observation).
+__device__ __forceinline__ int act_obs_bf(const float LDSP *fc, const float LDSP *fm,
+                                          float LDSP *key, uint16_t LDSP *ord,
+                                          int32_t LDSP *stk, int P, float vc, float vm) {
+  const int lane = lane_id();
+  float best = -INFINITY;
+  int cnt = 0, bi = -1;
+  for (int i = lane; i < P; i += 64) {
+    if (fc[i] + vc <= 1.0f && fm[i] + vm <= 1.0f) {
+      const float k = fc[i] + fm[i];
+      if (k > best) {
+        best = k;
+        cnt = 1;
+        bi = i;
+      } else if (k == best) {
+        cnt++;
+      }
+    }
+  }
+  float m = best;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  int tot = (best == m) ? cnt : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  if (tot == 0) return -1;
+  if (tot == 1) {
+    const uint64_t who = ballot(best == m && cnt == 1);
+    return __builtin_amdgcn_readlane(bi, __ffsll((unsigned long long)who) - 1);
+  }
+  int above = 0, eq = 0;
+  for (int i = lane; i < P; i += 64) {
+    const float k = fc[i] + fm[i];
+    key[i] = k;
+    ord[i] = (uint16_t)i;
+    above += fless(m, k);
+    eq += k == m;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    above += __shfl_xor(above, o);
+    eq += __shfl_xor(eq, o);
+  }
+  const int hi = P - above - 1, lo = P - above - eq;
+  wsync();
+  wave_aquicksort(key, ord, P, stk, lo, hi, reinterpret_cast<uint16_t LDSP *>(stk + 256));
+  wsync();
+  for (int b = hi; b >= lo; b -= 64) {  // visiting order: descending positions
+    const int pos = b - lane;
+    const int q = pos >= lo ? (int)ord[pos] : 0;
+    const uint64_t f = ballot(pos >= lo && fc[q] + vc <= 1.0f && fm[q] + vm <= 1.0f);
+    if (f) return __builtin_amdgcn_readlane(q, __ffsll((unsigned long long)f) - 1);
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(64) void k_act_obs(int P, int V, int policy, const float *obs,
+                                                int32_t *act) {
+  extern __shared__ __align__(16) char lds[];
+  float LDSP *fc = reinterpret_cast<float LDSP *>((char LDSP *)lds);
+  float LDSP *fm = fc + P;
+  float LDSP *key = fm + P;
+  int32_t LDSP *stk = reinterpret_cast<int32_t LDSP *>(key + P);
+  uint16_t LDSP *ord = reinterpret_cast<uint16_t LDSP *>(stk + 256 + P);  // after the scratch
+  const int lane = lane_id(), e = blockIdx.x;
+  const int D = 3 * V + 2 * P;
+  const float *o = obs + (int64_t)e * D;
+  int32_t *a = act + (int64_t)e * V;
+  for (int i = lane; i < P; i += 64) {
+    fc[i] = o[3 * V + i];
+    fm[i] = o[3 * V + P + i];
+  }
+  wsync();
+  const float wait = (float)P;
+  for (int b = 0; b < V; b += 64) {
+    const int v = b + lane;
+    const float pl = v < V ? o[v] : 0.f;
+    const float vc = v < V ? o[V + v] : 0.f, vm = v < V ? o[2 * V + v] : 0.f;
+    int out = (int)pl;  // action = np.copy(vm_placement)
+    uint64_t todo = ballot(v < V && pl == wait);
+    while (todo) {
+      const int l = __ffsll((unsigned long long)todo) - 1;
+      todo &= todo - 1;
+      const float c = __shfl(vc, l), m = __shfl(vm, l);
+      int q = -1;
+      if (policy == 0) {  // firstfit.py:33-37: first PM in index order
+        for (int i0 = 0; i0 < P && q < 0; i0 += 64) {
+          const int i = i0 + lane;
+          const uint64_t f = ballot(i < P && fc[i] + c <= 1.0f && fm[i] + m <= 1.0f);
+          if (f) q = i0 + __ffsll((unsigned long long)f) - 1;
+        }
+      } else {  // bestfit.py:33-39
+        q = act_obs_bf(fc, fm, key, ord, stk, P, c, m);
+      }
+      if (q >= 0) {
+        if (lane == l) out = q;
+        wsync();
+        if (lane == 0) {
+          fc[q] = fc[q] + c;
+          if (policy != 0) fm[q] = fm[q] + m;  // FirstFit leaves memory (firstfit.py:36)
+        }
+        wsync();
+      }
+    }
+    if (v < V) a[v] = out;
+  }
+}
+
 }  // namespace vmp

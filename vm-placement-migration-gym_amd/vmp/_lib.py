@@ -14,12 +14,13 @@ POLICIES = {"firstfit": 0, "bestfit": 1}
 EXPORTS = (
     "vmp_abi_version", "vmp_last_error", "vmp_create", "vmp_destroy", "vmp_set_stream",
     "vmp_set_eval", "vmp_dims", "vmp_reset", "vmp_step", "vmp_heuristic_act",
+    "vmp_heuristic_act_obs",
     "vmp_heuristic_step", "vmp_rollout_heuristic", "vmp_mask", "vmp_mask_bool", "vmp_get_obs",
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
     "vmp_policy_head", "vmp_policy_head_backward", "vmp_policy_head_backward_bf16",
     "vmp_actor_head", "vmp_record_enable",
     "vmp_record_read",
-    "vmp_debug_stamps",
+    "vmp_debug_fail_alloc", "vmp_debug_stamps",
 )
 
 
@@ -75,6 +76,7 @@ def lib():
         "vmp_reset": (ctypes.c_int, [P, P, P, P]),
         "vmp_step": (ctypes.c_int, [P, P, P, P, P, P]),
         "vmp_heuristic_act": (ctypes.c_int, [P, i32, P]),
+        "vmp_heuristic_act_obs": (ctypes.c_int, [P, i32, P, P]),
         "vmp_heuristic_step": (ctypes.c_int, [P, i32, P, P, P, P, P]),
         "vmp_rollout_heuristic": (ctypes.c_int, [P, i32, i32, P, P]),
         "vmp_mask": (ctypes.c_int, [P, P]),
@@ -93,12 +95,13 @@ def lib():
                                            P, P, P, P, P, P, P]),
         "vmp_record_enable": (ctypes.c_int, [P, i32]),
         "vmp_record_read": (ctypes.c_int, [P, P, P]),
+        "vmp_debug_fail_alloc": (ctypes.c_int, [i32]),
         "vmp_debug_stamps": (ctypes.c_int, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 6:
+    if L.vmp_abi_version() != 7:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

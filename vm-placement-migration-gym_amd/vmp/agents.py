@@ -2,9 +2,8 @@
 
 Reference: src/agents/base.py:13-136 (Base: set_log / test / record_testing_step),
 src/agents/firstfit.py:21-38 and src/agents/bestfit.py:21-40. Same constructor
-signatures and methods; act() runs the heuristic scan in the HIP kernel on the
-env's current state (vmp_heuristic_act), which is the observation the Base.test
-loop passes in.
+signatures and methods; act(observation) runs the heuristic scan in a HIP
+kernel on the observation it is given (vmp_heuristic_act_obs).
 """
 from dataclasses import asdict, dataclass, is_dataclass
 from time import gmtime, strftime
@@ -68,7 +67,12 @@ class Base:
         """base.py:63-118: one eval episode (eval_steps) from reset(seed=config.seed),
         every step recorded; returns the Record (saved to `output` if given). The
         Record metrics are accumulated on the device during the episode
-        (vmp_record_*); the host keeps the per-step traces of the JSON."""
+        (vmp_record_*); the host keeps the per-step traces of the JSON. Each
+        call starts a fresh Record (the reference appends the traces of every
+        call while replacing vm_arrival_steps, so a second test() would pair
+        two episodes' placements with one episode's arrivals): the saved
+        traces and the summary always describe the same episode."""
+        self.record.clear()
         self.env.eval()
         self.eval()
         obs, info = self.env.reset(seed=self.env.config.seed)
@@ -144,10 +148,14 @@ class _HeuristicAgent(Base):
         pass
 
     def act(self, observation):
-        """The heuristic's action on the env's current observation -> int64 [V]
-        (or [N, V] for a BatchedVmEnv)."""
+        """The heuristic's action computed from `observation` -> int64 [V] (or
+        [N, V] for a BatchedVmEnv's [N, D] observations), as the reference
+        reads only the obs it is passed (firstfit.py:22-28): an edited or stale
+        observation gets its own action, not the env's. The scan runs in the
+        HIP kernel (vmp_heuristic_act_obs); Base.test's fused act+step path
+        (vmp_heuristic_step) acts on the env state, which is that obs."""
         b = batched_env(self.env)
-        a = b.heuristic_act(self.POLICY).cpu().numpy().astype(np.int64)
+        a = b.heuristic_act_obs(observation, self.POLICY).cpu().numpy().astype(np.int64)
         return a[0] if b is not self.env else a
 
 

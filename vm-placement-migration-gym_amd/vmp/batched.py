@@ -124,6 +124,17 @@ class BatchedVmEnv:
         check(lib().vmp_heuristic_act(h, _lib.POLICIES[policy], ptr(a)))
         return a
 
+    def heuristic_act_obs(self, obs, policy="firstfit"):
+        """FirstFitAgent.act / BestFitAgent.act on the given observations (any
+        f32 [N, D], not necessarily the envs' own; firstfit.py:21-38,
+        bestfit.py:21-40) -> int32 [N, V]. Reads no env state."""
+        h = self._bind()
+        o = torch.as_tensor(obs, dtype=torch.float32, device=self.device).reshape(
+            self.n_envs, self.D).contiguous()
+        a = self._empty((self.n_envs, self.V), torch.int32)
+        check(lib().vmp_heuristic_act_obs(h, _lib.POLICIES[policy], ptr(o), ptr(a)))
+        return a
+
     def heuristic_step(self, policy="firstfit", want_actions=False, want_valid=False,
                        want_obs=True):
         """act(obs) then step(action) in one launch (the Base.test loop body)."""

@@ -77,14 +77,30 @@ def ortho_init(layer, scale=np.sqrt(2)):
 
 
 def _bf16_weight(w):
-    """bf16 copy of a parameter, made once per parameter version: AdamW's
-    in-place step bumps `_version`, so the copy is refreshed once per optimizer
-    step instead of at every forward of every update chunk."""
+    """bf16 copy of a parameter in ONE buffer per parameter (fixed address),
+    refreshed in place once per parameter version: AdamW's in-place step bumps
+    `_version`, so the cast runs once per optimizer step instead of at every
+    forward of every update chunk. Under HIP-graph capture the cast is always
+    recorded (the graph re-casts the live parameter on every replay), and the
+    buffer is never reallocated while a graph may read it. Writes that bypass
+    the version counter (`p.data` broadcasts) must call _bf16_invalidate."""
     c = getattr(w, "_vmp_bf16", None)
-    if c is None or c[0] != w._version or c[1].shape != w.shape:
-        c = (w._version, w.detach().to(torch.bfloat16))
+    if c is None or c[1].shape != w.shape or c[1].device != w.device:
+        c = [None, torch.empty(w.shape, dtype=torch.bfloat16, device=w.device)]
         w._vmp_bf16 = c
+    capturing = w.is_cuda and torch.cuda.is_current_stream_capturing()
+    if capturing or c[0] != w._version:
+        c[1].copy_(w.detach())
+        if not capturing:  # a captured copy does not run now: keep the stamp
+            c[0] = w._version
     return c[1]
+
+
+def _bf16_invalidate(params):
+    for p in params:
+        c = getattr(p, "_vmp_bf16", None)
+        if c is not None:
+            c[0] = None
 
 
 _ADDMM_OUT_DTYPE = None
@@ -223,7 +239,8 @@ class Network(nn.Module):
         last = self.actor[-1]
         return (self._head is H.policy_head and self.precision == "f32" and obs.is_cuda
                 and obs.dtype == torch.float32 and H.actor_head_preferred(self.V, self.A)
-                and H.actor_head_supported(last.weight, last.weight, self.A))
+                and last.weight.dtype == torch.float32 and last.in_features % 32 == 0
+                and self.A <= H.ACTOR_HEAD_MAX_A)
 
     def sample(self, obs, bits=None, wait_ratio=-1.0, wait_index=-1):
         """Rollout sampling (ppo.py:115-126 with the mask as packed bits; the WAIT
@@ -484,6 +501,7 @@ class PPOTrainer:
     def _sync_params(self):
         for p in self.model.parameters():
             self.dist.broadcast(p.data, src=0, group=self.group)
+        _bf16_invalidate(self.model.parameters())  # p.data writes keep `_version`
 
     def _allreduce(self, t):
         if self.dist:
@@ -669,15 +687,22 @@ class PPOTrainer:
         return stats
 
     def _chunk_bytes(self, dev):
-        """Logits budget per update chunk: PPOConfig.chunk_bytes, or 1/8 of the
-        device's memory (36 GB on a 288 GB MI355X: a whole config/100.yml
-        minibatch of 8192 envs, 25 GB of f32 logits, is one chunk, so backward
-        writes each gradient once instead of accumulating chunk by chunk)."""
+        """Logits budget per update chunk: PPOConfig.chunk_bytes, or what the
+        device can hold now: a chunk's peak is its f32 logits, the dlogits of
+        the backward and the saved activations (<= 3x the logits), so the
+        budget is a third of the memory free on the device (incl. blocks torch
+        has cached but not handed out), capped at 1/8 of the device. On an idle
+        288 GB MI355X that is 36 GB: a whole config/100.yml minibatch of 8192
+        envs (25 GB of f32 logits) is one chunk, so backward writes each
+        gradient once instead of accumulating chunk by chunk; on a smaller or
+        shared GPU the chunks shrink instead of running out of memory."""
         if int(self.cfg.chunk_bytes) > 0:
             return int(self.cfg.chunk_bytes)
         if dev.type != "cuda":
             return 4 << 30
-        return int(torch.cuda.get_device_properties(dev).total_memory) // 8
+        free, total = torch.cuda.mem_get_info(dev)
+        free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        return max(1 << 28, min(int(total) // 8, int(free) // 3))
 
     def _zero_grads(self, params):
         """Single process: grads re-created by backward. Data parallel: every

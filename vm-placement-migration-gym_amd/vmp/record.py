@@ -8,8 +8,16 @@ vmp_record_read, csrc/vmp_record.hip) and `summary_from_device` turns the
 recorder's sums and rate histograms into get_summary()'s dict. `Record` keeps
 the reference's attribute names for the per-step traces Base.test appends, so
 save() writes the JSON layout plots.ipynb and the exp_* drivers read, and its
-summary is the device one. (The literal host restatement of record.py lives in
-tests/record_literal.py, where it checks the device recorder.)
+summary is the device one.
+
+A Record with no device summary (filled through record_testing_step by a
+caller's own loop, or re-imported from JSON) derives the same metrics from its
+traces on the host (`_life_table`: cumulative counts over the [step, slot]
+placement matrix, evaluated at every life's bounds at once), and exposes the
+reference's metric properties (pending_rates, slowdown_rates, vm_lifetime,
+drop_rate, total_rewards, unique_vms_placement) on either path, as the
+exp_* drivers read them (exp_performance.py:104-105, exp_suspension.py:56-59).
+(tests/record_literal.py restates record.py literally and checks both.)
 """
 import json
 import os
@@ -41,9 +49,93 @@ class Record:
             setattr(self, k, [])
         self._device = None  # summary_from_device(...) of the recorded episode
 
+    def clear(self):
+        """Drop the traces and the device summary (Base.test starts each episode
+        with this, so a saved record holds one episode and its own summary)."""
+        for k in TRACE_KEYS:
+            setattr(self, k, [])
+        self._device = None
+
     def set_device_summary(self, summary):
         """Attach the recorder's summary of the episode (Base.test does this)."""
         self._device = dict(summary)
+
+    # ---- the reference's metric properties (record.py:33-108), host side ----
+    def _lives(self):
+        return _life_table(self.vm_placements, self.vm_arrival_steps, self.WAIT_STATUS)
+
+    @property
+    def unique_vms_placement(self):
+        """record.py:33-51: each VM life's existing-state placements."""
+        H = np.asarray(self.vm_placements)
+        out = []
+        for slot, lo, hi in zip(*_life_bounds(self.vm_arrival_steps, len(H))):
+            col = H[lo:hi, slot]
+            out.append(col[col <= self.WAIT_STATUS])
+        return out
+
+    @property
+    def pending_rates(self):
+        """record.py:54-66: (first running index + 1) / life length, 1.0 if none."""
+        return _pending(*self._lives())
+
+    @property
+    def slowdown_rates(self):
+        """record.py:68-83: waiting steps after the first run / remaining life."""
+        return _slowdown(*self._lives())
+
+    @property
+    def vm_lifetime(self):
+        """record.py:85-96: steps after the first run, 0 if the VM never ran."""
+        return _lifetime(*self._lives())
+
+    @property
+    def drop_rate(self):
+        """record.py:98-102: dropped / requested per step (0 where none)."""
+        d = np.asarray(self.dropped_requests, dtype=float)
+        t = np.asarray(self.total_requests, dtype=float)
+        return np.divide(d, t, out=np.zeros(d.shape, dtype=float), where=t != 0)
+
+    @property
+    def total_rewards(self):
+        """record.py:104-108: rewards below -1e7 replaced by the mean of those above."""
+        if self._device is not None and not self.rewards:
+            return self._device["total rewards"]
+        r = np.array(self.rewards, dtype=float)
+        low = r < -1e7
+        if low.any():
+            r[low] = r[r > -1e7].mean()
+        return np.round(r.sum(), 3)
+
+    def host_summary(self):
+        """get_summary() (record.py:110-134) computed from the traces."""
+        lives = self._lives()
+        pend, slow, life = _pending(*lives), _slowdown(*lives), _lifetime(*lives)
+        rnd = lambda x: np.round(x, 3)  # noqa: E731
+        return {
+            "total rewards": self.total_rewards,
+            "total served VMs": self.served_requests[-1],
+            "total requests": self.total_requests[-1],
+            "total cpu requested": rnd(self.total_cpu_requested),
+            "total memory requested": rnd(self.total_memory_requested),
+            "total suspend actions": self.suspended[-1],
+            "total place actions": self.placed[-1],
+            "average VM life": rnd(np.mean(life)),
+            "average pending": rnd(np.mean(pend)),
+            "median pending": rnd(np.median(pend)),
+            "max pending": rnd(np.max(pend)) if pend else 0,
+            "average slowdown": rnd(np.mean(slow)),
+            "median slowdown": rnd(np.median(slow)),
+            "max slowdown": rnd(np.max(slow)),
+            "drop rate": rnd(np.mean(self.drop_rate)),
+            "cpu mean": rnd(np.mean(self.cpu)),
+            "cpu mean target": rnd(np.mean(self.target_cpu_mean)),
+            "cpu std": rnd(np.std(self.cpu)),
+            "memory mean": rnd(np.mean(self.memory)),
+            "memory mean target": rnd(np.mean(self.target_memory_mean)),
+            "memory std": rnd(np.std(self.memory)),
+            "rank mean": rnd(np.mean(self.rank)),
+        }
 
     @property
     def device_summary(self):
@@ -51,11 +143,13 @@ class Record:
         return self._device
 
     def get_summary(self):
-        """record.py:110-134: same keys, same rounding; values from the device."""
-        if self._device is None:
-            raise RuntimeError("no recorded episode: run Base.test on the GPU env (the metrics "
-                               "are accumulated on the device) or import a saved record")
-        return {k: self._device[k] for k in SUMMARY_KEYS}
+        """record.py:110-134: same keys, same rounding; from the device recorder
+        when Base.test attached its summary, else from the traces."""
+        if self._device is not None:
+            return {k: self._device[k] for k in SUMMARY_KEYS}
+        if not self.vm_placements:
+            raise RuntimeError("empty record: no device summary and no recorded steps")
+        return self.host_summary()
 
     def save(self, path: str):
         """record.py:136-142: vars(self) as JSON, incl. `summary`."""
@@ -69,14 +163,82 @@ class Record:
 
     @classmethod
     def import_record(cls, agent: str, jsondict: dict):
-        """record.py:144-168: the traces of a saved record, and its saved summary."""
+        """record.py:144-168: the traces of a saved record; the summary is
+        recomputed from them as the reference does (the saved `summary` is used
+        only when the JSON holds no per-step traces)."""
         r = cls(agent, jsondict["env_config"], jsondict.get("agent_config"))
         for k in TRACE_KEYS:
             if k in jsondict:
                 setattr(r, k, jsondict[k])
-        if "summary" in jsondict:
+        if "summary" in jsondict and not r.vm_placements:
             r.set_device_summary(jsondict["summary"])
         return r
+
+
+# Per-life metrics from _life_table's (n, f, w). The reference tests
+# `if allocated_at:`, so a first run at index 0 counts as "never ran" (f <= 0).
+def _pending(n, f, w):
+    return [float(x) for x in np.where(f > 0, np.around((f + 1.0) / np.maximum(n, 1), 3), 1.0)]
+
+
+def _slowdown(n, f, w):
+    ran = f > 0
+    rest = (n - f - 1)[ran]
+    rates = np.where(rest == 0, 0.0, np.around(w[ran] / np.maximum(rest, 1), 3))
+    return [float(x) for x in rates] if rates.size else [0]
+
+
+def _lifetime(n, f, w):
+    return [int(x) for x in np.where(f > 0, n - f - 1, 0)]
+
+
+def _life_bounds(arrival_steps, n_steps):
+    """(slot, lo, hi) of every VM life: the placement history is recorded from
+    timestep 2, so the life that starts at arrival step a begins at row a - 2;
+    a slot's first life starts at row 0 and its last ends at the last row."""
+    slots, lo, hi = [], [], []
+    for v, arr in enumerate(arrival_steps):
+        if not arr:
+            continue
+        cuts = [0] + [int(a) - 2 for a in arr[1:]] + [n_steps]
+        slots += [v] * (len(cuts) - 1)
+        lo += cuts[:-1]
+        hi += cuts[1:]
+    return (np.asarray(slots, dtype=np.int64), np.asarray(lo, dtype=np.int64),
+            np.asarray(hi, dtype=np.int64))
+
+
+def _life_table(placements, arrival_steps, wait, chunk=256):
+    """Per VM life: n = its existing-state entries (placement <= WAIT), f = the
+    index among them of the first running entry (< WAIT; -1 if none) and w =
+    the WAIT entries from that one on. Cumulative counts over the [step, slot]
+    matrix, taken `chunk` slots at a time, are read at every life's bounds."""
+    H = np.asarray(placements)
+    T = H.shape[0]
+    slots, lo, hi = _life_bounds(arrival_steps, T)
+    n = np.zeros(slots.size, dtype=np.int64)
+    f = np.full(slots.size, -1, dtype=np.int64)
+    w = np.zeros(slots.size, dtype=np.int64)
+    rows = np.arange(T + 1)[:, None]
+    for c0 in range(0, H.shape[1], chunk):
+        sel = (slots >= c0) & (slots < c0 + chunk)
+        if not sel.any():
+            continue
+        blk = H[:, c0:c0 + chunk]
+        zero = np.zeros((1, blk.shape[1]), dtype=np.int64)
+        ex = np.concatenate([zero, np.cumsum(blk <= wait, axis=0)])
+        wt = np.concatenate([zero, np.cumsum(blk == wait, axis=0)])
+        # next running row at or after each row (T where none)
+        run_at = np.where(blk < wait, rows[:-1], T)
+        nxt = np.concatenate([np.minimum.accumulate(run_at[::-1], axis=0)[::-1],
+                              np.full((1, blk.shape[1]), T)])
+        s, a, b = slots[sel] - c0, lo[sel], hi[sel]
+        n[sel] = ex[b, s] - ex[a, s]
+        r0 = nxt[a, s]
+        ran = r0 < b
+        f[sel] = np.where(ran, ex[np.minimum(r0, T), s] - ex[a, s], -1)
+        w[sel] = np.where(ran, wt[b, s] - wt[np.minimum(r0, T), s], 0)
+    return n, f, w
 
 
 class NpEncoder(json.JSONEncoder):
