@@ -43,23 +43,27 @@ CFG = dict(pms=100, vms=1000, arrival_rate=1.8182, service_length=1000, training
            cap_target_util=True, beta=0.5, allow_null_action=True)
 
 
-def step_bytes(P, V, words):
+def step_bytes(P, V, words, pms):
     """Algorithmic HBM bytes per env-step of the per-step kernel:
-    state read (8 B/VM word, 16 B/PM, 256 B header), obs f32[3V+2P], PM and
-    header write, reward f64, done u8, and the VM words that changed (`words`
-    per env-step: a running VM's word holds its finish key and is not rewritten
-    while it runs)."""
+    state read (8 B/VM word, 16 B/PM, 256 B header), obs f32[3V+2P], header
+    write, reward f64, done u8, the VM words that changed (`words` per
+    env-step: a running VM's word holds its finish key and is not rewritten
+    while it runs) and the PMs that changed (`pms` per env-step, cpu + memory
+    f64: only the PM words a place / suspend / free wrote are stored back)."""
     state = 8 * V + 16 * P + 256
-    return state + 4 * (3 * V + 2 * P) + 16 * P + 256 + 8 + 1 + 8 * words
+    return state + 4 * (3 * V + 2 * P) + 256 + 8 + 1 + 8 * words + 16 * pms
 
 
 def changed_words(c0, c1, env_steps):
-    """VM words written per env-step between two counter snapshots
+    """(VM words, PMs) written per env-step between two counter snapshots
     ([total_requests, served, suspend, place, dropped, timestep] per env):
-    accepted arrivals + finishers + placements + suspensions. An upper bound:
-    a slot freed and refilled in the same step is written once, counted twice."""
+    words = accepted arrivals + finishers + placements + suspensions, PMs =
+    finishers + placements + suspensions (each event writes one PM's cpu and
+    memory). Upper bounds: a slot freed and refilled in the same step is
+    written once, and several events on one PM write it once."""
     d = (c1 - c0).double().sum(0)
-    return float((d[0] - d[4] + d[1] + d[2] + d[3]) / env_steps)
+    return (float((d[0] - d[4] + d[1] + d[2] + d[3]) / env_steps),
+            float((d[1] + d[2] + d[3]) / env_steps))
 
 
 def main():
@@ -170,7 +174,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    words = changed_words(c_before, env.counters(), N * K)  # after the clock stops
+    words, pmw = changed_words(c_before, env.counters(), N * K)  # after the clock stops
     kern_ms = ev0.elapsed_time(ev1) / K
     if dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
@@ -249,7 +253,7 @@ def main():
                    "sample": f"{n_cpu} envs x {steps_cpu} FirstFit act+step after {warm_cpu} "
                              f"warm-up steps, OpenMP {threads} threads (C oracle, same config)"}
 
-    bpe = step_bytes(P, V, words)
+    bpe = step_bytes(P, V, words, pmw)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
@@ -287,7 +291,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "vmp::k_env<16, true> (heuristic act+step, one step per launch)", "kernel_ms": kern_ms,
-                     "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words},
+                     "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
+                     "pms_written_per_env_step": pmw},
         "cpu_baseline": cpu,
         "reference_cpu": _reference_cpu(),
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},
@@ -374,12 +379,12 @@ def bench_period(args, dev, rank, world, dist, cfg):
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
     c1 = env.counters()
-    words = changed_words(c0, c1, N * K)
+    words, pmw = changed_words(c0, c1, N * K)
     ms = np.array([a.elapsed_time(b) for a, b in ev])
     env.close()
     mean_ms = _max_over_ranks(float(ms.mean()), dev, dist)
     bins = [round(float(ms[i:i + 100].mean()), 4) for i in range(0, K, 100)]
-    bpe = step_bytes(P, V, words)
+    bpe = step_bytes(P, V, words, pmw)
     ach = bpe * N / (mean_ms * 1e-3) / 1e9
     return {"value": world * N / (mean_ms * 1e-3), "unit": "env-steps/s",
             "value_kind": "mean per-launch kernel time over the window",
@@ -388,6 +393,7 @@ def bench_period(args, dev, rank, world, dist, cfg):
             "steps": K, "mean_ms": mean_ms, "max_ms": float(ms.max()),
             "min_ms": float(ms.min()), "ms_by_100_steps": bins,
             "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
+            "pms_written_per_env_step": pmw,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS,
                          "kernel": "vmp::k_env<16, true> (heuristic act+step)"}}
@@ -439,10 +445,10 @@ def bench_nominal(args, dev, rank, world, dist):
     if dist:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
-    words = changed_words(c0, env.counters(), N * K)
+    words, pmw = changed_words(c0, env.counters(), N * K)
     kern_ms = _max_over_ranks(ev0.elapsed_time(ev1) / K, dev, dist)
     env.close()
-    bpe = step_bytes(P, V, words)
+    bpe = step_bytes(P, V, words, pmw)
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -460,6 +466,7 @@ def bench_nominal(args, dev, rank, world, dist):
             "envs_per_gpu": N, "ff_steps": ff_total, "steps": K, "mean_running": running,
             "mean_waiting": waiting, "ms_per_step": 1e3 * el / K, "kernel_ms": kern_ms,
             "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
+            "pms_written_per_env_step": pmw,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS,
                          "kernel": "vmp::k_env<16, true> (heuristic act+step)"},
@@ -572,10 +579,10 @@ def bench_stress(args, dev, rank, world, dist):
     if dist:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
-    words = changed_words(c_before, env.counters(), N * K)
+    words, pmw = changed_words(c_before, env.counters(), N * K)
     kern_ms = _max_over_ranks(ev0.elapsed_time(ev1) / K, dev, dist)
     env.close()
-    bpe = step_bytes(P, V, words)
+    bpe = step_bytes(P, V, words, pmw)
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
             "workload": "P1000 V10000, lambda 1.818, L 1000, reward kl, BestFit act + step "
@@ -583,6 +590,7 @@ def bench_stress(args, dev, rank, world, dist):
             "ff_steps": args.stress_ff, "steps": K, "mean_running": running,
             "mean_waiting": waiting, "ms_per_step": 1e3 * el / K, "kernel_ms": kern_ms,
             "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
+            "pms_written_per_env_step": pmw,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS, "kernel": "vmp::k_env_big<20, true>"}}
 
@@ -629,14 +637,15 @@ def bench_external(args, env, dev, stream, dist, world, P, V):
     if dist:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
-    words = changed_words(c_before, env.counters(), N * K)
+    words, pmw = changed_words(c_before, env.counters(), N * K)
     kern_ms = _max_over_ranks(float(np.mean([a.elapsed_time(b) for a, b in ev])), dev, dist)
-    bpe = step_bytes(P, V, words) + 4 * V
+    bpe = step_bytes(P, V, words, pmw) + 4 * V
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     return {"value": world * N / (kern_ms * 1e-3), "unit": "env-steps/s",
             "value_kind": "step kernel alone (events around vmp_step)",
             "act_plus_step_wall": world * N * K / el, "steps": K, "kernel_ms": kern_ms,
             "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
+            "pms_written_per_env_step": pmw,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": ach / HBM_PEAK_GBS,
                          "kernel": "vmp::k_env_ext<16> (external actions)"}}

@@ -276,6 +276,9 @@ int vmp_record_read(vmp_handle *h, uint32_t *hist, double *sums);
  * failure and cleanup paths of vmp_create / vmp_record_enable / vmp_mask_bool
  * under the host sanitizers (tests/native/capi_faults.cpp). */
 int vmp_debug_fail_alloc(int32_t n);
+/* Number of device allocations the library currently holds (all handles):
+ * back to its previous value after a failed call or a vmp_destroy. */
+int64_t vmp_debug_live_allocs(void);
 
 /* Diagnostics: per-env shader-clock cycles per kernel phase, accumulated since
  * the previous call, device u64[n_env][24] (see tools/stamps.py for the phase names).

@@ -14,7 +14,8 @@
 //   with a device (`capi_faults --device`, the GPU box): for every n, the
 //   n-th device allocation of vmp_create / vmp_record_enable / vmp_mask_bool
 //   fails (vmp_debug_fail_alloc) and the call returns VMP_EOOM with nothing
-//   leaked (host: LeakSanitizer; device: free memory back to its start), the
+//   leaked (host: LeakSanitizer; device: the library's live-allocation count,
+//   vmp_debug_live_allocs, back to its value before the call), the
 //   handle stays usable after a failed vmp_record_enable, and a full create /
 //   step / record / destroy cycle runs clean.
 #include <hip/hip_runtime.h>
@@ -123,46 +124,69 @@ static size_t free_mem() {
   return fr;
 }
 
-static void device_faults() {
-  vmp_config c = base_cfg();
-  std::vector<int64_t> seeds(64);
-  for (int i = 0; i < 64; i++) seeds[i] = 4 * i;
-  vmp_handle *h = nullptr;
-  // warm the runtime (first allocations map pools), then take the baseline
-  CHECK(vmp_create(&c, 64, seeds.data(), 0, &h) == VMP_OK, "warm create");
-  CHECK(vmp_destroy(h) == VMP_OK, "warm destroy");
-  CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
-  const size_t base = free_mem();
+// One sweep: the n-th device allocation of vmp_create fails, for every n up to
+// the first n past the last allocation. Returns the number of failure points.
+static int create_sweep(const vmp_config &c, std::vector<int64_t> &seeds) {
   int n_fail = 0;
   for (int n = 1; n < 64; n++) {
     CHECK(vmp_debug_fail_alloc(n) == VMP_OK, "arm");
-    h = nullptr;
-    int rc = vmp_create(&c, 64, seeds.data(), 0, &h);
+    vmp_handle *h = nullptr;
+    const int64_t live = vmp_debug_live_allocs();
+    const int rc = vmp_create(&c, (int32_t)seeds.size(), seeds.data(), 0, &h);
     vmp_debug_fail_alloc(0);
+    if (rc != VMP_OK) CHECK(vmp_debug_live_allocs() == live, "no device allocation kept");
     if (rc == VMP_OK) {
       CHECK(h != nullptr, "handle");
       vmp_destroy(h);
-      std::printf("ok  create: allocation %d is past the last one (%d failure points)\n", n,
-                  n - 1);
       break;
     }
     CHECK(rc == VMP_EOOM, "create under injected OOM returns VMP_EOOM");
     CHECK(h == nullptr, "no handle on failure");
     n_fail++;
   }
-  CHECK(n_fail >= 5, "vmp_create has its allocations behind dev_malloc");
   CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
-  CHECK(free_mem() >= base, "device memory back after the failed creates");
+  return n_fail;
+}
+
+static void device_faults() {
+  vmp_config c = base_cfg();
+  // large enough that a leaked buffer shows in the free memory (vm words
+  // 9.8 MB, PM state 6.6 MB, headers 1 MB at 4096 envs)
+  std::vector<int64_t> seeds(4096);
+  for (size_t i = 0; i < seeds.size(); i++) seeds[i] = 4 * (int64_t)i;
+  vmp_handle *h = nullptr;
+  // warm the runtime (code objects, pools) with one full sweep, then measure
+  // the free device memory across three more: a leak on any failure path
+  // grows it by at least one buffer per sweep
+  const int n_fail = create_sweep(c, seeds);
+  CHECK(n_fail >= 5, "vmp_create has its allocations behind dev_malloc");
+  const size_t base = free_mem();
+  const int64_t live0 = vmp_debug_live_allocs();
+  for (int r = 0; r < 3; r++) CHECK(create_sweep(c, seeds) == n_fail, "same failure points");
+  // exact: the library's own count of live device allocations; the runtime's
+  // free-memory figure is printed for context (it keeps freed blocks cached)
+  std::printf("ok  create: %d failure points; live device allocations %lld -> %lld; free device "
+              "memory %zu -> %zu bytes over 3 sweeps\n", n_fail, (long long)live0,
+              (long long)vmp_debug_live_allocs(), base, free_mem());
+  CHECK(vmp_debug_live_allocs() == live0 && live0 == 0, "device allocations back to none");
   // record_enable / mask_bool on a live handle
   CHECK(vmp_create(&c, 64, seeds.data(), 0, &h) == VMP_OK, "create");
+  for (int n = 1; n <= 9; n++) {  // warm: the recorder's first allocations
+    vmp_debug_fail_alloc(n);
+    (void)vmp_record_enable(h, 1);
+    vmp_debug_fail_alloc(0);
+  }
   const size_t with_handle = free_mem();
+  const int64_t live_h = vmp_debug_live_allocs();
   for (int n = 1; n <= 9; n++) {
     vmp_debug_fail_alloc(n);
     CHECK(vmp_record_enable(h, 1) == VMP_EOOM, "record_enable under injected OOM");
     vmp_debug_fail_alloc(0);
+    CHECK(vmp_debug_live_allocs() == live_h, "recorder buffers released after the failure");
   }
   CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
-  CHECK(free_mem() >= with_handle, "recorder buffers released after each failure");
+  std::printf("ok  record_enable: 9 failure points; free device memory %zu -> %zu bytes\n",
+              with_handle, free_mem());
   CHECK(vmp_record_enable(h, 1) == VMP_OK, "record_enable after the failures");
   float *obs = nullptr;
   double *rew = nullptr, *sums = nullptr;
@@ -178,12 +202,15 @@ static void device_faults() {
     CHECK(vmp_heuristic_step(h, VMP_POLICY_BESTFIT, nullptr, obs, rew, done, nullptr) == VMP_OK,
           "heuristic_step");
   CHECK(vmp_record_read(h, hist, sums) == VMP_OK, "record_read");
+  const int64_t live_r = vmp_debug_live_allocs();
   vmp_debug_fail_alloc(1);
   CHECK(vmp_mask_bool(h, mask) == VMP_EOOM, "mask_bool under injected OOM");
   vmp_debug_fail_alloc(0);
+  CHECK(vmp_debug_live_allocs() == live_r, "mask_bool failure keeps nothing");
   CHECK(vmp_mask_bool(h, mask) == VMP_OK, "mask_bool after the failure");
   CHECK(hipDeviceSynchronize() == hipSuccess, "kernels ran");
   CHECK(vmp_destroy(h) == VMP_OK, "destroy");
+  CHECK(vmp_debug_live_allocs() == 0, "destroy releases every device allocation");
   (void)hipFree(obs);
   (void)hipFree(rew);
   (void)hipFree(done);

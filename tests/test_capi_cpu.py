@@ -13,7 +13,7 @@ LIB = os.path.join(ROOT, "vm-placement-migration-gym_amd", "vmp", "libvmp.so")
 
 def declared():
     src = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(vmp_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(vmp_\w+)\s*\(", src, re.M)))
 
 
 def test_header_declares_entry_points():

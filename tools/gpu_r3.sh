@@ -4,8 +4,9 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out/${1:-r3}
 mkdir -p $OUT
-K=${2:+-k "$2"}
-eval timeout -k 10 700 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread $K > $OUT/gpu_tests.log 2>&1
+KARGS=()
+[ -n "$2" ] && KARGS=(-k "$2")
+timeout -k 10 700 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread "${KARGS[@]}" > $OUT/gpu_tests.log 2>&1
 rc=$?; echo "tests_rc=$rc"; tail -3 $OUT/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.log 2>&1
 rc=$?; echo "bench_rc=$rc"; tail -c 3000 $OUT/bench.log; exit $rc

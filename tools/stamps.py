@@ -1,5 +1,7 @@
 """Phase breakdown of the env kernel from a -DVMP_STAMPS build (diagnostic).
-Usage: VMP_LIB_PATH=.../libvmp_stamps.so python tools/stamps.py [envs] [vms]"""
+Usage: VMP_LIB_PATH=.../libvmp_stamps.so python tools/stamps.py [envs] [vms] [ff] [K]
+(ff fast-forward steps of phase-aligned envs, then K stamped steps: ff 2000
+times the refill burst, ff 2500 the quiet phase after it)"""
 import os
 import sys
 
@@ -18,12 +20,14 @@ cfg = Config(pms=100, vms=V, arrival_rate=1.8182, service_length=1000, training_
              eval_steps=100000, seed=0, reward_function="wr", allow_null_action=True)
 env = BatchedVmEnv(cfg, N)
 env.eval(os.environ.get("STAMP_TRAIN") is None)
-for _ in range(25):
+FF = int(sys.argv[3]) if len(sys.argv) > 3 else 2500
+for _ in range(FF // 100):
     env.rollout("firstfit", 100)
 NS = 24
 buf = torch.zeros((N, NS), dtype=torch.int64, device="cuda")
 _lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
-K = 50
+K = int(sys.argv[4]) if len(sys.argv) > 4 else 50
+c0 = env.counters().cpu().numpy()
 for _ in range(K):
     env.heuristic_step("firstfit")
 torch.cuda.synchronize()
@@ -35,7 +39,11 @@ names = ["loop-end", "act+apply(rest)", "run_vms", "accept", "stats(rest)+reward
          "pro:start->hdr/pm loaded", "pro:predraw", "pro:VM words loaded",
          "heur:prep", "heur:bitmaps", "heur:queries", "heur:apply", "-", "-", "-", "-"]
 tot = st.sum(1) - st[:, 7] - st[:, 9]
-print(f"N={N} V={V}: mean cycles per env-step (per wave) = {tot.mean():.0f}")
+c1 = env.counters().cpu().numpy()
+d = (c1 - c0).sum(0) / (N * K)
+print(f"N={N} V={V} steps {FF + 1}-{FF + K}: mean cycles per env-step (per wave) = "
+      f"{tot.mean():.0f}; per env-step: accepted {d[0] - d[4]:.3f}, finished {d[1]:.3f}, "
+      f"placed {d[3]:.3f}, suspended {d[2]:.3f}")
 for i in range(NS):
     if names[i] != "-":
         print(f"  {names[i]:20s} {st[:, i].mean():10.0f}  ({100 * st[:, i].mean() / tot.mean():5.1f}%)")

@@ -62,7 +62,10 @@ int fail(int code, const std::string &msg) {
 // Device allocations of the handle go through here, so the failure paths can
 // be exercised (vmp_debug_fail_alloc: the n-th allocation from now fails as
 // out-of-memory; tests/test_sanitizers_cpu.py, tests/native/capi_faults.cpp).
+// g_live counts the library's live device allocations (vmp_debug_live_allocs),
+// so a leak on a failure path is seen exactly, whatever the runtime caches.
 std::atomic<int64_t> g_fail_alloc{0};
+std::atomic<int64_t> g_live{0};
 template <class T>
 hipError_t dev_malloc(T **p, size_t bytes) {
   int64_t n = g_fail_alloc.load();
@@ -72,7 +75,15 @@ hipError_t dev_malloc(T **p, size_t bytes) {
     *p = nullptr;
     return hipErrorOutOfMemory;
   }
-  return hipMalloc(reinterpret_cast<void **>(p), bytes);
+  const hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+  if (e == hipSuccess && *p) g_live++;
+  else *p = nullptr;
+  return e;
+}
+void dev_free(void *p) {
+  if (!p) return;
+  (void)hipFree(p);
+  g_live--;
 }
 
 // random_loggam (numpy distributions.c), host copy for the PTRS table.
@@ -220,6 +231,10 @@ void carve(vmp_handle *h) {
   if (deep) off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);  // lo, len, lane-0 stack
   p.off_leafval = (int32_t)off;
   if (deep) off = align16(off + 8 * (2 * (int64_t)p.n_leaf + 64));  // leaf sums + value stack
+  // changed-PM bitmap (bit i: double i of cpu[P] | memory[P] was written this
+  // launch): only those PM words are stored back
+  p.off_pdirty = (int32_t)off;
+  off = align16(off + 8 * ((2 * P + 63) / 64));
   p.off_pre = (int32_t)off;   // per-launch random draws follow (launch_env)
   p.lds_wave_bytes = (int32_t)off;
 }
@@ -434,22 +449,22 @@ static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, cons
     e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
   }
-  (void)hipFree(dseeds);
+  dev_free(dseeds);
   if (e != hipSuccess) return fail(VMP_EDEVICE, std::string("vmp_create reset: ") + hipGetErrorString(e));
   return VMP_OK;
 }
 
 int vmp_destroy(vmp_handle *h) {
   if (!h) return VMP_OK;
-  (void)hipFree(h->vmw);
-  (void)hipFree(h->pm);
-  (void)hipFree(h->hdr);
-  (void)hipFree(h->lg_arr);
-  (void)hipFree(h->lg_svc);
-  (void)hipFree(h->scratch_bits);
-  (void)hipFree(h->pois_dev);
-  (void)hipFree(h->jump_dev);
-  (void)hipFree(h->stamps);
+  dev_free(h->vmw);
+  dev_free(h->pm);
+  dev_free(h->hdr);
+  dev_free(h->lg_arr);
+  dev_free(h->lg_svc);
+  dev_free(h->scratch_bits);
+  dev_free(h->pois_dev);
+  dev_free(h->jump_dev);
+  dev_free(h->stamps);
   vmp_record_enable(h, 0);
   delete h;
   return VMP_OK;
@@ -604,15 +619,15 @@ int vmp_record_enable(vmp_handle *h, int32_t on) {
   if (!h) return fail(VMP_EINVAL, "null handle");
   if (!on) {
     if (h->rec_on) (void)hipStreamSynchronize(h->stream);
-    (void)hipFree(h->rec.prev);
-    (void)hipFree(h->rec.life_n);
-    (void)hipFree(h->rec.alloc);
-    (void)hipFree(h->rec.waits);
-    (void)hipFree(h->rec.hist);
-    (void)hipFree(h->rec.sums);
-    (void)hipFree(h->rec_act);
-    (void)hipFree(h->rec_valid);
-    (void)hipFree(h->rec_reward);
+    dev_free(h->rec.prev);
+    dev_free(h->rec.life_n);
+    dev_free(h->rec.alloc);
+    dev_free(h->rec.waits);
+    dev_free(h->rec.hist);
+    dev_free(h->rec.sums);
+    dev_free(h->rec_act);
+    dev_free(h->rec_valid);
+    dev_free(h->rec_reward);
     std::memset(&h->rec, 0, sizeof(h->rec));
     h->rec_act = nullptr;
     h->rec_valid = nullptr;
@@ -731,6 +746,8 @@ int vmp_get_rank(vmp_handle *h, int64_t *rank) {
   HIP_TRY(hipGetLastError());
   return VMP_OK;
 }
+
+int64_t vmp_debug_live_allocs(void) { return g_live.load(); }
 
 int vmp_debug_fail_alloc(int32_t n) {
   if (n < 0) return fail(VMP_EINVAL, "n must be >= 0");

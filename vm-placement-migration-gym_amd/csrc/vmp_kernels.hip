@@ -722,6 +722,7 @@ struct Lds {
   uint64_t LDSP *svcfb;              // rng4 state for fallback draws
   int32_t LDSP *svcinfo;             // [0] speculative count, [1] consumed
   uint8_t LDSP *ccomp, *mcomp;  // compressed sizes of existing VMs [V]
+  uint64_t LDSP *pdirty;             // bit i: PM double i (cpu | memory) changed
   PwLds pw;
   char LDSP *base;                   // the wave's LDS region
 };
@@ -751,6 +752,7 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   L.svcst = reinterpret_cast<uint64_t LDSP *>(base + p.off_pre);
   L.svc = reinterpret_cast<uint32_t LDSP *>(base + p.off_pre + 16 * p.scap);
   L.arr = reinterpret_cast<int32_t LDSP *>(base + p.off_pre + 20 * p.scap);
+  L.pdirty = reinterpret_cast<uint64_t LDSP *>(base + p.off_pdirty);
   L.ccomp = reinterpret_cast<uint8_t LDSP *>(base + p.off_ccomp);
   L.mcomp = L.ccomp + p.V;
   L.pw.lo = reinterpret_cast<int32_t LDSP *>(base + p.off_leaf);
@@ -1007,9 +1009,17 @@ __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int k
   return -1;
 }
 
+// Record that PM q's cpu and memory were written (one lane: the callers'
+// writes are single-lane); the state store writes back only marked PM words.
+__device__ __forceinline__ void mark_pm(const Lds &L, int P, int q) {
+  L.pdirty[q >> 6] |= 1ull << (q & 63);
+  L.pdirty[(P + q) >> 6] |= 1ull << ((P + q) & 63);
+}
+
 // One VM placement event of the env (env.py:74-84 for a WAIT -> PM move):
 // _resource_valid in f64, then _place_vm. Returns validity (wave-uniform).
-__device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int q, int kc, int km) {
+__device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int P, int q, int kc,
+                                          int km) {
   double cq = L.cpu[q], mq = L.mem[q];
   double vc = T.cent[kc], vm = T.cent[km];
   bool ok = (cq + vc <= 1) && (mq + vm <= 1);
@@ -1017,6 +1027,7 @@ __device__ __forceinline__ bool env_place(const Lds &L, const Tables &T, int q, 
   if (ok && lane_id() == 0) {
     L.cpu[q] = cq + vc;
     L.mem[q] = mq + vm;
+    mark_pm(L, P, q);
   }
   wsync();
   return ok;
@@ -1310,7 +1321,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
       hit &= pend;
       const int kc = w_cc(ww), km = w_cm(ww);
       const int q = bf ? bf_choose(p, L, kc, km) : bm_query(L, NW, kc, km);  // wave-uniform
-      const bool ok = env_place(L, T, q, kc, km);  // env.py:55-56, 58-64
+      const bool ok = env_place(L, T, P, q, kc, km);  // env.py:55-56, 58-64
       n_place += ok;
       if (lane == wl) {
 #pragma unroll
@@ -1429,6 +1440,7 @@ __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L,
       if (lane == 0) {
         L.cpu[q] = cq;
         L.mem[q] = mq;
+        mark_pm(L, P, q);
       }
       okm |= (uint64_t)eok << l;
       wsync();
@@ -1504,6 +1516,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
       if (lane == 0) {
         L.cpu[q] = cq;
         L.mem[q] = mq;
+        mark_pm(L, P, q);
       }
       wsync();
     }
@@ -1823,6 +1836,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   for (int j = 0; j < 4; j++)
     if (j * 64 + lane < n_pm) L.cpu[j * 64 + lane] = pv[j];
   for (int i = 256 + lane; i < n_pm; i += 64) L.cpu[i] = pm[i];  // P > 128
+  for (int i = lane; i < (n_pm + 63) / 64; i += 64) L.pdirty[i] = 0;
   wsync();
 #ifdef VMP_STAMPS
   __shared__ uint64_t st_lds[kEnvWavesPerBlock * kStamps];
@@ -1913,8 +1927,12 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
         }
       }
     }
+    // only the PM words written this launch (place / suspend / free: the
+    // precision clamp changes no other value, as every stored value is 0 or
+    // >= 1e-7 after the previous launch's clamp)
     double *pmo = p.pm + (int64_t)e * 2 * P;
-    for (int i = lane; i < 2 * P; i += 64) ST_NT(pmo + i, (double)L.cpu[i]);
+    for (int i = lane, j = 0; i < 2 * P; i += 64, j++)
+      if ((L.pdirty[j] >> lane) & 1ull) ST_NT(pmo + i, (double)L.cpu[i]);
     if (lane < 32)
       gptr(reinterpret_cast<uint64_t *>(p.hdr + e))[lane] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane];
   }
@@ -2373,7 +2391,7 @@ VMP_SLOOP
       STAMP(18);
       if (w0) {
         const int q = bf ? bf_choose(p, L, kc, km) : bm_query(L, NW, kc, km);
-        const bool ok = env_place(L, T, q, kc, km);
+        const bool ok = env_place(L, T, P, q, kc, km);
         const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
         wsync();
         if (lane == 0) {
@@ -2498,6 +2516,7 @@ VMP_SLOOP
         if (lane == 0) {
           L.cpu[q] = cq;
           L.mem[q] = mq;
+          mark_pm(L, P, q);
           B.evok[i] = (uint8_t)eok;
         }
         wsync();
@@ -2710,9 +2729,10 @@ __device__ __forceinline__ void big_store(const EnvParams &p, const Lds &L, cons
       ST_NT(obs + 3 * V + i, (float)L.cpu[i]);
       ST_NT(obs + 3 * V + P + i, (float)L.mem[i]);
     }
-  if (state) {
+  if (state) {  // the PM words written this launch (as env_body's store)
     double *pmo = p.pm + (int64_t)e * 2 * P;
-    for (int i = t; i < 2 * P; i += NT) ST_NT(pmo + i, (double)L.cpu[i]);
+    for (int i = t; i < 2 * P; i += NT)
+      if ((L.pdirty[i >> 6] >> (i & 63)) & 1ull) ST_NT(pmo + i, (double)L.cpu[i]);
   }
 }
 
@@ -2798,6 +2818,7 @@ VMP_SLOOP
         if (lane == 0) {
           L.cpu[q] = cq;
           L.mem[q] = mq;
+          mark_pm(L, P, q);
         }
         wsync();
       }
@@ -2968,6 +2989,7 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   for (int j = 0; j < 4; j++)
     if (j * NT + t < n_pm) L.cpu[j * NT + t] = pv[j];
   for (int i = 4 * NT + t; i < n_pm; i += NT) L.cpu[i] = pm[i];  // P > 2 * NT
+  for (int i = t; i < (n_pm + 63) / 64; i += NT) L.pdirty[i] = 0;
   for (int i = t; i < kBigMaxSPT * kBigMaxWaves; i += NT) B.rc[i] = 0;
   uint32_t rem[SPT];
 #pragma unroll

@@ -74,7 +74,7 @@ struct EnvParams {
   int32_t off_hdr, off_pm, off_fpm, off_thr, off_ord, off_bits, off_sort, off_ccomp;
   int32_t off_leaf, off_leafval, off_stage, off_pre;
   int32_t scap;    // speculative service draws per launch
-  int32_t pad1;
+  int32_t off_pdirty;  // u64[ceil(2P/64)]: PM doubles (cpu then memory) changed this launch
   // PCG64 jump table: entry j = (A, M) with state after j+1 draws = A*s + M*inc
   // (A = a^(j+1), M = sum_{i<=j} a^i mod 2^128), u64 [64][4] {A.hi, A.lo, M.hi, M.lo}
   const uint64_t *jump;
