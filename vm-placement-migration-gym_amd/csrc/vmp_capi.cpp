@@ -214,11 +214,8 @@ void carve(vmp_handle *h) {
   off = align16(off + 2 * P);            // tc, tm u8
   p.off_ord = (int32_t)off;
   off = align16(off + 2 * P);            // BF visiting order u16
-  p.off_bits = (int32_t)off;  // fit bitmaps; after the heuristic: NULL list + accepted sizes
-  {
-    const int64_t bits = 2 * 101 * 8 * (int64_t)p.NW, acc = 4 * V;
-    off = align16(off + (bits > acc ? bits : acc));
-  }
+  p.off_bits = (int32_t)off;  // any-fit table (u32[128]); after the heuristic: NULL list + accepted sizes
+  off = align16(off + (4 * V > 512 ? 4 * V : 512));
   p.off_stage = (int32_t)off;
   off = align16(off + 8 * 16);           // reduction results + draw bookkeeping
   // ccomp, mcomp u8 (stats, after the action phase) share their region with

@@ -52,6 +52,23 @@ __device__ __forceinline__ T GLBP *gptr(T *p) {
 
 // ------------------------------------------------------------ wave utils --
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// An LDS base the compiler cannot tie to earlier address arithmetic: the
+// pointers make_lds derives from it at a late use are recomputed there instead
+// of being kept live (and spilled) from the prologue.
+__device__ __forceinline__ char LDSP *opaque_base(char LDSP *b) {
+  uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)b);  // 32-bit
+  asm volatile("" : "+s"(x));
+  return (char LDSP *)(uintptr_t)x;
+}
+// The lane id recomputed where the compiler cannot tie it to lane_id(): slot
+// indices s*64 + lane built from it in a late phase (the obs / state stores)
+// are not the prologue's, which the register allocator otherwise keeps live
+// (spilled to scratch) from the loads at entry to the stores at exit.
+__device__ __forceinline__ int fresh_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 __device__ __forceinline__ int below(uint64_t m, int lane) {
@@ -711,7 +728,7 @@ struct Lds {
   float LDSP *fkey;                  // BF keys fcpu + fmem
   uint8_t LDSP *tc, *tm;        // per-PM largest fitting size (hundredths), f32 semantics
   uint16_t LDSP *ord;                // BF ascending argsort, then reversed into visiting order
-  uint64_t LDSP *bc, *bm;       // [101][NW] fit bitmaps by size (bit = visiting position)
+  uint64_t LDSP *bc, *bm;       // action phase: the any-fit table (u32 [128] at bc)
   int32_t LDSP *sortstk;             // introsort stacks
   uint16_t LDSP *nulls;              // NULL slot indices (aliases the fit bitmaps)
   uint8_t LDSP *accc, *accm;    // accepted sizes (alias the fit bitmaps)
@@ -844,55 +861,14 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int l) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Rebuild the fit bitmaps: bit i of bc[k][w] is set iff the PM at visiting
-// position w*64+i accepts a VM of cpu size k/100 (f32 obs arithmetic), i.e.
-// iff its threshold tc >= k. PMs are bucketed by threshold with LDS atomic
-// ORs, then an OR-scan over k turns buckets into "tc >= k" masks. Rows are
-// mapped to lanes in reverse (row 63-i, and row 127-i for rows 64..100) so
-// the suffix over k is a DPP prefix scan over lanes.
-__device__ __forceinline__ void build_bitmaps(const EnvParams &p, const Lds &L, bool bf) {
-  const int lane = lane_id();
-  const int P = p.P, NW = p.NW;
-  for (int i = lane; i < 101 * NW; i += 64) {
-    L.bc[i] = 0;
-    L.bm[i] = 0;
-  }
-  wsync();
-  for (int w = 0; w < NW; w++) {
-    const int pos = w * 64 + lane;
-    if (pos < P) {
-      const int q = bf ? (int)L.ord[pos] : pos;
-      const int tcq = (int)L.tc[q] - 1, tmq = (int)L.tm[q] - 1;
-      if (tcq >= 0) __atomic_fetch_or(&L.bc[tcq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
-      if (tmq >= 0) __atomic_fetch_or(&L.bm[tmq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
-    }
-  }
-  wsync();
-  const int rlo = 63 - lane, rhi = 127 - lane;
-  const bool hi_ok = rhi <= 100;
-  for (int w = 0; w < NW; w++) {
-    uint64_t c1 = hi_ok ? L.bc[rhi * NW + w] : 0, m1 = hi_ok ? L.bm[rhi * NW + w] : 0;
-    uint64_t c0 = L.bc[rlo * NW + w], m0 = L.bm[rlo * NW + w];
-    c1 = prefix_or64(c1);
-    m1 = prefix_or64(m1);
-    c0 = prefix_or64(c0) | readlane_u64(c1, 63);
-    m0 = prefix_or64(m0) | readlane_u64(m1, 63);
-    L.bc[rlo * NW + w] = c0;
-    L.bm[rlo * NW + w] = m0;
-    if (hi_ok) {
-      L.bc[rhi * NW + w] = c1;
-      L.bm[rhi * NW + w] = m1;
-    }
-  }
-  wsync();
-}
-
-// Exact any-fit pre-check (the heuristics' common no-placement case): M[k] =
-// max of the +1-encoded memory thresholds tm over the PMs whose cpu threshold
-// is >= k (0: none). A VM of sizes (kc, km) fits some PM iff M[kc] > km, the
-// same predicate as "some fit bitmap bit is set" (firstfit.py:33,
-// bestfit.py:35: cpu and memory both fit). Rows reversed over the lanes as in
-// build_bitmaps, so the suffix max over k is a lane prefix max.
+// The any-fit table: M[k] = max of the +1-encoded memory thresholds tm over
+// the PMs whose cpu threshold is >= k (0: none). A VM of sizes (kc, km) fits
+// some PM iff M[kc] > km (firstfit.py:33, bestfit.py:35: cpu and memory both
+// fit). Built per step and after each placement (only the placed PM's
+// thresholds move); the heuristics' choices are then wave scans over the
+// thresholds (ff_scan, bf_choose). Levels are mapped to lanes in reverse
+// (row 63-i, and 127-i for levels 64..100), so the suffix max over k is a
+// DPP lane prefix max.
 __device__ __forceinline__ void build_fitmax(const EnvParams &p, const Lds &L, uint32_t LDSP *M) {
   const int lane = lane_id();
   M[lane] = 0;
@@ -914,31 +890,18 @@ __device__ __forceinline__ void build_fitmax(const EnvParams &p, const Lds &L, u
   wsync();
 }
 
-// First visiting position accepting sizes (kc, km), or -1.
-__device__ __forceinline__ int bm_query(const Lds &L, int NW, int kc, int km) {
-  if (NW <= 2) {  // P <= 128: both words at once, no early exit
-    const uint64_t a0 = L.bc[kc * NW] & L.bm[km * NW];
-    const uint64_t a1 = NW == 2 ? (L.bc[kc * NW + 1] & L.bm[km * NW + 1]) : 0ull;
-    return a0 ? __ffsll((unsigned long long)a0) - 1
-              : (a1 ? 64 + __ffsll((unsigned long long)a1) - 1 : -1);
-  }
-  for (int w = 0; w < NW; w++) {
-    uint64_t m = L.bc[kc * NW + w] & L.bm[km * NW + w];
-    if (m) return w * 64 + __ffsll((unsigned long long)m) - 1;
+// FirstFit's PM for sizes (kc, km) (firstfit.py:33-37): the first PM in index
+// order whose f32 thresholds accept both, by a wave scan over the PMs' u8
+// thresholds (P/64 ballots; no fit bitmaps to build or maintain). -1 if none.
+__device__ __forceinline__ int ff_scan(const EnvParams &p, const Lds &L, int kc, int km) {
+  const int lane = lane_id();
+  for (int b = 0; b < p.P; b += 64) {
+    const int i = b + lane;
+    const bool f = i < p.P && (int)L.tc[i] - 1 >= kc && (int)L.tm[i] - 1 >= km;
+    const uint64_t m = ballot(f);
+    if (m) return b + __ffsll((unsigned long long)m) - 1;
   }
   return -1;
-}
-
-// Does any visiting position accept sizes (kc, km)? No early exit, so the
-// row reads of all words are in flight together (latency of one LDS round trip
-// per 8 words instead of one per word).
-__device__ __forceinline__ bool bm_any(const Lds &L, int NW, int kc, int km) {
-  const uint64_t LDSP *rc = L.bc + kc * NW;
-  const uint64_t LDSP *rm = L.bm + km * NW;
-  uint64_t acc = 0;
-#pragma unroll 8
-  for (int w = 0; w < NW; w++) acc |= rc[w] & rm[w];
-  return acc != 0;
 }
 
 // BestFit's choice for sizes (kc, km) (bestfit.py:33-39): the first PM in
@@ -1261,7 +1224,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
                                                    int policy, int32_t *act_out,
                                                    uint8_t *valid_out STAMP_PARAMS) {
   const int lane = lane_id();
-  const int P = p.P, WAIT = p.P, NW = p.NW;
+  const int P = p.P, WAIT = p.P;
   const bool bf = policy == 1;
   uint32_t pend = 0;
 #pragma unroll
@@ -1279,25 +1242,18 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     }
     wsync();
     STAMP(16);
-    // which pending VMs fit some PM, from the any-fit table; the fit bitmaps
-    // are built only if one does
     uint32_t hit = 0;  // bit s: VM slot s of this lane is pending and some PM fits it
-    {
-      uint32_t LDSP *M = reinterpret_cast<uint32_t LDSP *>(L.bc);
-      build_fitmax(p, L, M);
+    // the any-fit table M (build_fitmax) answers "does some PM accept (c, m)";
+    // it is rebuilt after each placement (only the placed PM's thresholds move)
+    uint32_t LDSP *M = reinterpret_cast<uint32_t LDSP *>(L.bc);
+    build_fitmax(p, L, M);
 #pragma unroll
-      for (int s = 0; s < VPT; s++)
-        hit |= (uint32_t)(((pend >> s) & 1u) && M[w_cc(wa[s])] > (uint32_t)w_cm(wa[s])) << s;
-    }
+    for (int s = 0; s < VPT; s++)
+      hit |= (uint32_t)(((pend >> s) & 1u) && M[w_cc(wa[s])] > (uint32_t)w_cm(wa[s])) << s;
     const bool anyfit = ballot(hit != 0) != 0;
-    bool rebuild = true;
+    STAMP(17);
 #pragma unroll 1
     for (; anyfit;) {
-      if (rebuild) {  // single site: the initial build (index-order fit bitmaps)
-        build_bitmaps(p, L, false);
-        rebuild = false;
-        STAMP(17);
-      }
       // earliest VM (index order) with a fit
       int ws = -1, wl = 0;
       uint32_t ww = 0;
@@ -1320,7 +1276,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         if (s < ws || (s == ws && lane <= wl)) pend &= ~(1u << s);
       hit &= pend;
       const int kc = w_cc(ww), km = w_cm(ww);
-      const int q = bf ? bf_choose(p, L, kc, km) : bm_query(L, NW, kc, km);  // wave-uniform
+      const int q = bf ? bf_choose(p, L, kc, km) : ff_scan(p, L, kc, km);  // wave-uniform
       const bool ok = env_place(L, T, P, q, kc, km);  // env.py:55-56, 58-64
       n_place += ok;
       if (lane == wl) {
@@ -1347,37 +1303,26 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
         }
       }
       wsync();
-      {  // only PM q's bits change (cpu row; BF also the memory row)
+      {
         const int t = (int)L.tc[q] - 1;
         const int tmq = (int)L.tm[q] - 1;
-        const int w = q >> 6;
-        const uint64_t bit = 1ull << (q & 63);
-        for (int k = lane; k < 101; k += 64) {
-          const uint64_t x = L.bc[k * NW + w];
-          L.bc[k * NW + w] = (t >= k) ? (x | bit) : (x & ~bit);
-          if (bf) {
-            const uint64_t y = L.bm[k * NW + w];
-            L.bm[k * NW + w] = (tmq >= k) ? (y | bit) : (y & ~bit);
-          }
-        }
-        wsync();
+        build_fitmax(p, L, M);
         // re-query the VMs q fitted before and not after
 #pragma unroll
         for (int s = 0; s < VPT; s++) {
           const int c = w_cc(wa[s]), m = w_cm(wa[s]);
           const bool rq = ((hit >> s) & 1u) && c <= tc_old && m <= tm_old && !(c <= t && m <= tmq);
-          if (ballot(rq)) {
-            if (rq && bm_query(L, NW, c, m) < 0) hit &= ~(1u << s);
-          }
+          if (rq && !(M[c] > (uint32_t)m)) hit &= ~(1u << s);
         }
       }
       STAMP(19);
     }
   }
   if (act_out || valid_out) {
+    const int ln = fresh_lane();
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
-      const int v = s * 64 + lane;
+      const int v = s * 64 + ln;
       if (live(wa[s])) {
         if (act_out && !((won >> s) & 1u)) gptr(act_out)[v] = (int32_t)w_pl(wa[s]);
         if (valid_out) gptr(valid_out)[v] = (uint8_t)!((bad >> s) & 1u);
@@ -1701,7 +1646,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
 template <int VPT>
 __device__ __forceinline__ void write_obs(const EnvParams &p, const Lds &L, const Tables &T,
                                           const uint32_t (&wa)[VPT], float *obs) {
-  const int lane = lane_id();
+  const int lane = fresh_lane();
   const int V = p.V, P = p.P;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
@@ -1722,7 +1667,7 @@ __device__ __forceinline__ void write_obs(const EnvParams &p, const Lds &L, cons
 template <int VPT>
 __device__ __forceinline__ void write_mask(const EnvParams &p, const Lds &L, const Tables &T,
                                            const uint32_t (&wa)[VPT], uint32_t *bits) {
-  const int lane = lane_id();
+  const int lane = fresh_lane();
   const int P = p.P, A = p.A, W = p.W32, WAIT = p.P, NUL = p.P + 1;
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
@@ -1876,7 +1821,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     else
       external_apply<VPT>(p, L, T, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
     STAMP(1);
-    if (ONE) {
+    if (ONE) {  // the time words' last use: bit s = slot s finishes this step if it runs
       const uint32_t t32 = (uint32_t)L.hdr->timestep;
 #pragma unroll
       for (int s = 0; s < VPT; s++) {  // by the placement before the action phase
@@ -1895,7 +1840,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     if (o.reward && lane == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
-  if (o.k_steps > 0) svc_commit(L);
+  if (o.k_steps > 0) svc_commit(make_lds(p, opaque_base(base)));
   if (!EXT && o.k_steps == 0 && o.policy >= 0 && o.act_out) {
     // act only: decide on a scratch copy of the VM words; nothing is stored
     uint32_t wt[VPT];
@@ -1911,9 +1856,10 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     if (o.done && lane == 0) gptr(o.done)[e] = (uint8_t)term;
     if (o.done_count && lane == 0) gptr(o.done_count)[e] += ndone;
     const uint32_t t32 = (uint32_t)(L.hdr->timestep - 1);  // this launch's step
+    const int ln = fresh_lane();
 #pragma unroll
     for (int s = 0; s < VPT; s++) {
-      const int v = s * 64 + lane;
+      const int v = s * 64 + ln;
       if (live(wa[s]) && ((dirty >> s) & 1u)) {  // unchanged words stay as they are
         if (!ONE) {
           ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rem[s] << 32));
@@ -2273,46 +2219,6 @@ __device__ __forceinline__ int block_min_int(int x, BigShared &B) {
   return s;
 }
 
-// build_bitmaps (index order) by the whole block: the words w of every
-// bitmap row are dealt to the waves, which own them through all three passes.
-// Barriers at entry (the thresholds tc / tm are written by other waves) and exit.
-__device__ __forceinline__ void big_build_bitmaps(const EnvParams &p, const Lds &L) {
-  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
-  const int wid = t >> 6, nwv = NT >> 6;
-  const int P = p.P, NW = p.NW;
-  for (int i = t; i < 101 * NW; i += NT) {
-    L.bc[i] = 0;
-    L.bm[i] = 0;
-  }
-  __syncthreads();
-  for (int w = wid; w < NW; w += nwv) {
-    const int pos = w * 64 + lane;
-    if (pos < P) {
-      const int tcq = (int)L.tc[pos] - 1, tmq = (int)L.tm[pos] - 1;
-      if (tcq >= 0) __atomic_fetch_or(&L.bc[tcq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
-      if (tmq >= 0) __atomic_fetch_or(&L.bm[tmq * NW + w], 1ull << lane, __ATOMIC_RELAXED);
-    }
-  }
-  wsync();  // the words of a wave are its own from here on
-  const int rlo = 63 - lane, rhi = 127 - lane;
-  const bool hi_ok = rhi <= 100;
-  for (int w = wid; w < NW; w += nwv) {
-    uint64_t c1 = hi_ok ? L.bc[rhi * NW + w] : 0, m1 = hi_ok ? L.bm[rhi * NW + w] : 0;
-    uint64_t c0 = L.bc[rlo * NW + w], m0 = L.bm[rlo * NW + w];
-    c1 = prefix_or64(c1);
-    m1 = prefix_or64(m1);
-    c0 = prefix_or64(c0) | readlane_u64(c1, 63);
-    m0 = prefix_or64(m0) | readlane_u64(m1, 63);
-    L.bc[rlo * NW + w] = c0;
-    L.bm[rlo * NW + w] = m0;
-    if (hi_ok) {
-      L.bc[rhi * NW + w] = c1;
-      L.bm[rhi * NW + w] = m1;
-    }
-  }
-  __syncthreads();
-}
-
 // FirstFit / BestFit act fused with the action phase (heuristic_apply, block form).
 template <int SPT>
 __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &L, const Tables &T,
@@ -2320,7 +2226,7 @@ __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &
                                                  int32_t *act_out, uint8_t *valid_out STAMP_PARAMS) {
   const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
   const bool w0 = t < 64;
-  const int P = p.P, WAIT = p.P, NW = p.NW;
+  const int P = p.P, WAIT = p.P;
   const bool bf = policy == 1;
   uint32_t pend = 0;
 VMP_SLOOP
@@ -2336,44 +2242,43 @@ VMP_SLOOP
       L.tc[i] = (uint8_t)(fit_threshold(fcv) + 1);
       L.tm[i] = (uint8_t)(fit_threshold(fmv) + 1);
     }
-    bool rebuild = true;
+    // the any-fit table M (build_fitmax, block form) answers "does some PM
+    // accept (c, m)" for the pending VMs; only the placed PM's thresholds move,
+    // so it is rebuilt after each placement (no fit bitmaps: FirstFit's choice
+    // is a wave scan over the u8 thresholds, BestFit's is bf_choose)
+    uint32_t *M = B.fmax;
+    auto build_m = [&]() {
+      for (int i = t; i < 128; i += NT) M[i] = 0;  // NT may be 64
+      __syncthreads();
+      for (int q = t; q < P; q += NT) {
+        const int tcq = (int)L.tc[q];
+        if (tcq > 0) __atomic_fetch_max(&M[tcq - 1], (uint32_t)L.tm[q], __ATOMIC_RELAXED);
+      }
+      __syncthreads();
+      if (w0) {
+        const int rlo = 63 - lane, rhi = 127 - lane;
+        const bool hi_ok = rhi <= 100;
+        uint32_t c1 = hi_ok ? M[rhi] : 0u, c0 = M[rlo];
+        c1 = prefix_max32(c1);
+        c0 = max(prefix_max32(c0), (uint32_t)__builtin_amdgcn_readlane((int)c1, 63));
+        wsync();
+        M[rlo] = c0;
+        if (hi_ok) M[rhi] = c1;
+      }
+      __syncthreads();
+    };
+    build_m();
+    STAMP(22);
     uint32_t hit = 0;
+VMP_SLOOP
+    for (int s = 0; s < SPT; s++)
+      if ((pend >> s) & 1u) {
+        const uint32_t w = W[s * NT + t];
+        if (M[w_cc(w)] > (uint32_t)w_cm(w)) hit |= 1u << s;
+      }
+    STAMP(17);
 #pragma unroll 1
     for (;;) {
-      if (rebuild) {
-        big_build_bitmaps(p, L);
-        STAMP(22);
-        // which pending VMs fit some PM: the any-fit table (build_fitmax), one
-        // LDS read per pending VM instead of a scan of its two bitmap rows
-        uint32_t *M = B.fmax;
-        for (int i = t; i < 128; i += NT) M[i] = 0;  // NT may be 64
-        __syncthreads();
-        for (int q = t; q < P; q += NT) {
-          const int tcq = (int)L.tc[q];
-          if (tcq > 0) __atomic_fetch_max(&M[tcq - 1], (uint32_t)L.tm[q], __ATOMIC_RELAXED);
-        }
-        __syncthreads();
-        if (w0) {
-          const int rlo = 63 - lane, rhi = 127 - lane;
-          const bool hi_ok = rhi <= 100;
-          uint32_t c1 = hi_ok ? M[rhi] : 0u, c0 = M[rlo];
-          c1 = prefix_max32(c1);
-          c0 = max(prefix_max32(c0), (uint32_t)__builtin_amdgcn_readlane((int)c1, 63));
-          wsync();
-          M[rlo] = c0;
-          if (hi_ok) M[rhi] = c1;
-        }
-        __syncthreads();
-        hit = 0;
-VMP_SLOOP
-        for (int s = 0; s < SPT; s++)
-          if ((pend >> s) & 1u) {
-            const uint32_t w = W[s * NT + t];
-            if (M[w_cc(w)] > (uint32_t)w_cm(w)) hit |= 1u << s;
-          }
-        rebuild = false;
-        STAMP(17);
-      }
       // earliest VM (index order) with a fit
       int mine = 0x7fffffff;
 VMP_SLOOP
@@ -2390,7 +2295,7 @@ VMP_SLOOP
       const int kc = w_cc(ww), km = w_cm(ww);
       STAMP(18);
       if (w0) {
-        const int q = bf ? bf_choose(p, L, kc, km) : bm_query(L, NW, kc, km);
+        const int q = bf ? bf_choose(p, L, kc, km) : ff_scan(p, L, kc, km);
         const bool ok = env_place(L, T, P, q, kc, km);
         const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
         wsync();
@@ -2403,23 +2308,6 @@ VMP_SLOOP
             L.fmem[q] = nm;
             L.tm[q] = (uint8_t)(fit_threshold(nm) + 1);
           }
-        }
-        wsync();
-        {  // only PM q's bits change (cpu row; BF also the memory row)
-          const int tq = (int)L.tc[q] - 1, tmq = (int)L.tm[q] - 1;
-          const int w = q >> 6;
-          const uint64_t bit = 1ull << (q & 63);
-          for (int k = lane; k < 101; k += 64) {
-            const uint64_t x = L.bc[k * NW + w];
-            L.bc[k * NW + w] = (tq >= k) ? (x | bit) : (x & ~bit);
-            if (bf) {
-              const uint64_t y = L.bm[k * NW + w];
-              L.bm[k * NW + w] = (tmq >= k) ? (y | bit) : (y & ~bit);
-            }
-          }
-          wsync();
-        }
-        if (lane == 0) {
           B.bc[1] = q;
           B.bc[2] = ok;
           B.bc[3] = tc_old;
@@ -2427,6 +2315,7 @@ VMP_SLOOP
           B.bc[5] = (int)L.tm[q] - 1;
           B.bc[7] = tm_old;
         }
+        wsync();
       }
       __syncthreads();
       STAMP(19);
@@ -2439,6 +2328,7 @@ VMP_SLOOP
         else bad |= 1u << ws;
         if (act_out) act_out[vw] = q;
       }
+      build_m();
       {  // re-query the VMs q fitted before and not after
         const int tq = B.bc[4], tc_old = B.bc[3], tmq = B.bc[5], tm_old = B.bc[7];
 VMP_SLOOP
@@ -2446,7 +2336,7 @@ VMP_SLOOP
           if (!((hit >> s) & 1u)) continue;
           const uint32_t w = W[s * NT + t];
           const int c = w_cc(w), m = w_cm(w);
-          if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && !bm_any(L, NW, c, m))
+          if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && !(M[c] > (uint32_t)m))
             hit &= ~(1u << s);
         }
       }
