@@ -333,3 +333,41 @@ def test_bf16_actor_head_node_equals_linear_plus_head(V, A):
     torch.testing.assert_close(gx1, gx2, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(gw1, gw2, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(gb1, gb2, rtol=1e-2, atol=1e-2 * gb2.abs().max().item())
+
+
+def test_bf16_graph_reads_the_live_parameters():
+    """a captured ActStepGraph in bf16 precision must act with the
+    parameters of the moment it is replayed. The bf16 weight copies live in one
+    buffer per parameter (fixed address) and the capture records the cast, so
+    after an optimizer-style in-place update and an eager forward (which
+    refreshes the copies eagerly), a replay's actions equal an uncaptured
+    act_batch with the new weights; so does a replay after a `p.data` write
+    (the data-parallel broadcast path, which bypasses `_version`)."""
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import ActStepGraph, PPOAgent, PPOConfig, _bf16_invalidate
+    cfg = Config(**dict(CFG10, arrival_rate=1.0, service_length=15, eval_steps=1000))
+    torch.manual_seed(0)
+    env = BatchedVmEnv(cfg, 128, device=DEV)
+    env.eval(True)
+    ag = PPOAgent(env, PPOConfig(hidden_size=64, masked=True, det=True, precision="bf16"))
+    ag.eval(True)
+    g = ActStepGraph(ag, warmup=1)
+    g.replay()
+    last = ag.model.actor[-1]
+    for how in ("step", "data"):
+        expect_old = ag.act_batch(g.obs.clone())
+        with torch.no_grad():
+            noise = torch.randn_like(last.weight) * 0.5
+            if how == "step":  # in place, as AdamW: bumps _version
+                last.weight.add_(noise)
+                ag.model.actor_logits(g.obs.clone())  # eager forward: refreshes the copy
+            else:  # a p.data write (dist.broadcast) + the trainer's invalidation
+                last.weight.data.add_(noise)
+                _bf16_invalidate(ag.model.parameters())
+        obs = g.obs.clone()
+        expect = ag.act_batch(obs)
+        assert not torch.equal(expect, expect_old), "the update should change some actions"
+        g.replay()
+        assert torch.equal(g.actions, expect), how
+    env.close()

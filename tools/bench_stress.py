@@ -55,6 +55,8 @@ def main():
     s = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
+    from bench import changed_words, step_bytes
+    c0 = env.counters()
     t0 = time.perf_counter()
     for a, b in ev:
         a.record(s)
@@ -63,7 +65,8 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    bpe = 2 * (8 * V + 16 * P + 256) + 4 * (3 * V + 2 * P) + 8 + 1
+    words, pms = changed_words(c0, env.counters(), N * args.steps)
+    bpe = step_bytes(P, V, words, pms)  # bench.py's byte model
     st = env.state()["vm_placement"]
     print(json.dumps({"workload": f"P{P} V{V} {args.policy} act+step, reward {args.reward}",
                       "envs": N, "value": N * args.steps / el, "unit": "env-steps/s",

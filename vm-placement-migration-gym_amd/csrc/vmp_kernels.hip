@@ -1347,6 +1347,7 @@ __device__ __forceinline__ void external_apply(const EnvParams &p, const Lds &L,
   // conditional load + wait per slot row
   const int32_t GLBP *ar = gptr(act_row);
   int32_t tv[VPT];
+  __asm__ volatile("" ::: "memory");  // not hoisted above the prologue's draws
 #pragma unroll
   for (int s = 0; s < VPT; s++) tv[s] = ar[min(s * 64 + lane, p.V - 1)];
 #pragma unroll
@@ -1772,14 +1773,24 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
 #ifdef VMP_STAMPS
   const uint64_t t_loaded = __builtin_amdgcn_s_memtime();
 #endif
+  // the external kernel parks the PM words in LDS before the draws (issued
+  // right behind the header, they are in by then): live across the draws
+  // they spilled to scratch there
+  if (EXT) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (j * 64 + lane < n_pm) L.cpu[j * 64 + lane] = pv[j];
+  }
   // the draws need only the header: they run while the PM / VM loads land
   if (o.k_steps > 0) predraw(p, L, T, o.k_steps, V, JA, JM);
 #ifdef VMP_STAMPS
   const uint64_t t_drawn = __builtin_amdgcn_s_memtime();
 #endif
+  if (!EXT) {
 #pragma unroll
-  for (int j = 0; j < 4; j++)
-    if (j * 64 + lane < n_pm) L.cpu[j * 64 + lane] = pv[j];
+    for (int j = 0; j < 4; j++)
+      if (j * 64 + lane < n_pm) L.cpu[j * 64 + lane] = pv[j];
+  }
   for (int i = 256 + lane; i < n_pm; i += 64) L.cpu[i] = pm[i];  // P > 128
   for (int i = lane; i < (n_pm + 63) / 64; i += 64) L.pdirty[i] = 0;
   wsync();
@@ -1799,7 +1810,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   uint32_t dirty = 0;  // bit s: this lane's VM word s changed (stored at the end)
   uint32_t fb = 0;     // ONE: bit s = slot s finishes this step if it runs
   uint32_t hiv[VPT];   // ONE: the finish keys / remaining runtimes, in flight
-  if (ONE) {
+  if (ONE && !EXT) {
     // issued before the action phase, consumed after it (latency hidden by it)
 #pragma unroll
     for (int s = 0; s < VPT; s++) hiv[s] = vlo[2 * min(s * 64 + lane, V - 1) + 1];
@@ -1818,8 +1829,16 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     for (int s = 0; s < VPT; s++) run0 |= (uint32_t)(w_pl(wa[s]) < P) << s;
     if (!EXT)
       n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row STAMP_ARGS);
-    else
+    else {
+      // the external kernel loads the time words after its action phase: live
+      // across it beside the 16 action words they spilled 10 VGPRs
       external_apply<VPT>(p, L, T, wa, o.actions + (int64_t)e * V, valid_row, n_place, n_susp);
+      if (ONE) {
+        const int ln = fresh_lane();
+#pragma unroll
+        for (int s = 0; s < VPT; s++) hiv[s] = vlo[2 * min(s * 64 + ln, V - 1) + 1];
+      }
+    }
     STAMP(1);
     if (ONE) {  // the time words' last use: bit s = slot s finishes this step if it runs
       const uint32_t t32 = (uint32_t)L.hdr->timestep;
@@ -2083,20 +2102,26 @@ __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, ui
 // applied by wave 0 in that order. Same arithmetic, same
 // order as k_env: the two kernels are interchangeable (VMP_BIG_KERNEL=1
 // forces this one for any V, which the parity tests use).
-// Slot-row loops of the block kernel (s = 0..SPT-1). Rolled: a full unroll
-// (-DVMP_BIG_UNROLL) hoists enough per-slot temporaries to grow the scratch
-// from 496 to 3296 B per lane at SPT = 20.
+// Slot-row loops of the block kernel (s = 0..SPT-1), unrolled by 4 (a full
+// unroll, -DVMP_BIG_UNROLL, hoists enough per-slot temporaries to grow the
+// scratch from 496 to 3296 B per lane at SPT = 20; -DVMP_BIG_ROLLED keeps one
+// row per iteration, one LDS round trip per row).
 #ifdef VMP_BIG_UNROLL
 #define VMP_SLOOP _Pragma("unroll")
-#else
+#elif defined(VMP_BIG_ROLLED)
 #define VMP_SLOOP _Pragma("unroll 1")
+#else  // 4 slot rows per iteration: 4 LDS reads in flight per round trip
+#define VMP_SLOOP _Pragma("unroll 4")
 #endif
 
 constexpr int kBigMaxSPT = 20, kBigMaxWaves = 8;
-// k_env_big's per-step helpers (pairwise-sum jobs, reward, draws): out of line
-// by default; -DVMP_BIG_CALL=__forceinline__ inlines them (A/B build)
+// k_env_big's per-step helpers (pairwise-sum jobs, reward, draws): inlined
+// (round 3: out of line, every call saved and restored the caller's live
+// registers through scratch, 224 B per lane; inlined the kernel needs 193
+// VGPRs instead of 250 and runs 8 % faster with the 4-row slot loops);
+// -DVMP_BIG_CALL=__noinline__ restores the calls (A/B build)
 #ifndef VMP_BIG_CALL
-#define VMP_BIG_CALL __noinline__
+#define VMP_BIG_CALL __forceinline__
 #endif
 struct BigShared {
   int32_t wcnt[16];   // per-wave counts of a compaction

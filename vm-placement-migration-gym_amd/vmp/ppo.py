@@ -325,6 +325,7 @@ class ActStepGraph:
         self.env.mask_bits(out=self.bits)
         a = self.agent.act_batch(self.obs, self.bits)
         self.env.step(a, obs=self.obs, reward=self.reward, done=self.done, want_valid=False)
+        self.actions = a  # the captured step's action buffer: the last replay's actions
 
     def replay(self):
         self.graph.replay()
