@@ -37,7 +37,8 @@ st = buf.cpu().numpy().astype(np.float64) / K
 names = ["loop-end", "act+apply(rest)", "run_vms", "accept", "stats(rest)+reward", "obs", "store",
          "-", "-", "-", "-", "stats:compress", "stats:pw-sums",
          "pro:start->hdr/pm loaded", "pro:predraw", "pro:VM words loaded",
-         "heur:prep", "heur:bitmaps", "heur:queries", "heur:apply", "-", "-", "-", "-"]
+         "heur:prep", "heur:fitmax+hits", "heur:earliest", "apply:requery", "apply:scan+place",
+         "apply:f32 update", "-", "apply:fitmax"]
 tot = st.sum(1) - st[:, 7] - st[:, 9]
 c1 = env.counters().cpu().numpy()
 d = (c1 - c0).sum(0) / (N * K)

@@ -1254,22 +1254,19 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     STAMP(17);
 #pragma unroll 1
     for (; anyfit;) {
-      // earliest VM (index order) with a fit
-      int ws = -1, wl = 0;
-      uint32_t ww = 0;
-#pragma unroll
-      for (int s = 0; s < VPT; s++) {
-        if (ws < 0) {
-          const uint64_t m = ballot((hit >> s) & 1u);
-          if (m) {
-            ws = s;
-            wl = __ffsll((unsigned long long)m) - 1;
-            ww = rdlane(wa[s], wl);
-          }
-        }
-      }
+      // earliest VM (index order s * 64 + lane) with a fit: each lane's lowest
+      // hit slot, then a DPP max over the wave of (2047 - index)
+      const int mine = hit ? (__builtin_ctz(hit) << 6) | lane : 2047;
+      const int best = 2047 - (int)__builtin_amdgcn_readlane(
+                                  (int)prefix_max32((uint32_t)(2047 - mine)), 63);
       STAMP(18);
-      if (ws < 0) break;
+      if (best == 2047) break;
+      const int ws = best >> 6, wl = best & 63;
+      uint32_t own = 0;
+#pragma unroll
+      for (int s = 0; s < VPT; s++)
+        if (s == ws) own = wa[s];
+      const uint32_t ww = rdlane(own, wl);
       // everything up to and including the winner is decided
 #pragma unroll
       for (int s = 0; s < VPT; s++)
@@ -1277,8 +1274,35 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
       hit &= pend;
       const int kc = w_cc(ww), km = w_cm(ww);
       const int q = bf ? bf_choose(p, L, kc, km) : ff_scan(p, L, kc, km);  // wave-uniform
-      const bool ok = env_place(L, T, P, q, kc, km);  // env.py:55-56, 58-64
+      // the env event (env.py:55-64: _resource_valid in f64, _place_vm) and the
+      // heuristic's own f32 update (FF: cpu only, firstfit.py:36) read and
+      // write disjoint state: one LDS round trip, one write-back
+      const double cq = L.cpu[q], mq = L.mem[q];
+      const float fq = L.fcpu[q], fmq = L.fmem[q];
+      const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
+      const double vc = T.cent[kc], vm = T.cent[km];
+      const bool ok = (cq + vc <= 1) && (mq + vm <= 1);
+      const float nc = fq + T.fcent[kc];
+      const float nm = fmq + T.fcent[km];
+      const int t = fit_threshold(nc);
+      const int tmq = bf ? fit_threshold(nm) : tm_old;
+      wsync();
+      if (lane == 0) {
+        if (ok) {
+          L.cpu[q] = cq + vc;
+          L.mem[q] = mq + vm;
+          mark_pm(L, P, q);
+        }
+        L.fcpu[q] = nc;
+        L.tc[q] = (uint8_t)(t + 1);
+        if (bf) {
+          L.fmem[q] = nm;
+          L.tm[q] = (uint8_t)(tmq + 1);
+        }
+      }
+      wsync();
       n_place += ok;
+      STAMP(20);
       if (lane == wl) {
 #pragma unroll
         for (int s = 0; s < VPT; s++)
@@ -1289,30 +1313,20 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
           }
         if (act_out) gptr(act_out)[ws * 64 + wl] = q;
       }
-      // heuristic state update (f32): FF updates cpu only (firstfit.py:36)
-      const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
-      wsync();
-      if (lane == 0) {
-        const float nc = L.fcpu[q] + T.fcent[kc];
-        L.fcpu[q] = nc;
-        L.tc[q] = (uint8_t)(fit_threshold(nc) + 1);
-        if (bf) {
-          const float nm = L.fmem[q] + T.fcent[km];
-          L.fmem[q] = nm;
-          L.tm[q] = (uint8_t)(fit_threshold(nm) + 1);
-        }
-      }
-      wsync();
-      {
-        const int t = (int)L.tc[q] - 1;
-        const int tmq = (int)L.tm[q] - 1;
+      STAMP(21);
+      if (t < tc_old || tmq < tm_old) {  // q's thresholds fell: the table changes
         build_fitmax(p, L, M);
-        // re-query the VMs q fitted before and not after
+        STAMP(23);
+        // re-query the VMs still pending with a fit (M is exact: "some PM
+        // accepts (c, m)"), table reads batched four slots at a time
 #pragma unroll
-        for (int s = 0; s < VPT; s++) {
-          const int c = w_cc(wa[s]), m = w_cm(wa[s]);
-          const bool rq = ((hit >> s) & 1u) && c <= tc_old && m <= tm_old && !(c <= t && m <= tmq);
-          if (rq && !(M[c] > (uint32_t)m)) hit &= ~(1u << s);
+        for (int s0 = 0; s0 < VPT; s0 += 4) {
+          uint32_t mc[4];
+#pragma unroll
+          for (int j = 0; j < 4; j++) mc[j] = s0 + j < VPT ? M[w_cc(wa[s0 + j])] : 0u;
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (s0 + j < VPT && !(mc[j] > (uint32_t)w_cm(wa[s0 + j]))) hit &= ~(1u << (s0 + j));
         }
       }
       STAMP(19);
