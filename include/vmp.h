@@ -286,6 +286,11 @@ int64_t vmp_debug_live_allocs(void);
  * returns VMP_EINVAL. */
 int vmp_debug_stamps(vmp_handle *h, uint64_t *out);
 
+/* Diagnostics: workgroups per CU the runtime reports for the per-step env
+ * kernel of this handle (hipOccupancyMaxActiveBlocksPerMultiprocessor) and
+ * the LDS bytes it is launched with (dynamic + static). */
+int vmp_debug_occupancy(vmp_handle *h, int32_t *blocks_per_cu, int32_t *lds_bytes);
+
 #ifdef __cplusplus
 }
 #endif

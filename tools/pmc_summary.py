@@ -1,5 +1,5 @@
 """Summarise tools/gpu_profile.sh output for the per-step env kernel.
-Usage: python tools/pmc_summary.py gpurun_out/prof [envs] [--write profiles/traffic.json]
+Usage: python tools/pmc_summary.py gpurun_out/prof [envs] [--write profiles/traffic.json] [--kernel NAME]
 
 Takes every dispatch of vmp::k_env<16, true> (the launch bench.py times) from the
 kernel trace and the counter passes, and reports the average duration and the
@@ -13,7 +13,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "k_env<16, true>"
+KERNEL = sys.argv[sys.argv.index("--kernel") + 1] if "--kernel" in sys.argv else "k_env<16, true>"
 d = sys.argv[1]
 N = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 32768
 vals = defaultdict(list)

@@ -22,13 +22,16 @@ template <int VPT, bool ONE>
 __global__ void k_env(EnvParams p, StepOut o);
 template <int VPT>
 __global__ void k_env_ext(EnvParams p, StepOut o);
-template <int SPT, bool ONE>
-__global__ void k_env_big(EnvParams p, StepOut o);
 __global__ void k_rank(EnvParams p, int64_t *rank);
 __global__ void k_target_means_lds(EnvParams p);
-constexpr int kBigMaxThreads = 512;  // k_env_big: one workgroup per env
-constexpr int kBigMaxV = 20 * kBigMaxThreads;
-constexpr int kBigStaticLds = 12 * 1024;  // Tables + BigShared
+// k_env_big: one workgroup per env; its geometry (threads, slots per thread)
+// and launcher live with the kernel (vmp_kernels.hip)
+void big_geometry(int *nt, int *spt_max);
+void launch_big_env(int spt, bool one, int n_env, size_t lds, hipStream_t s, const EnvParams &p,
+                    const StepOut &o);
+int big_occupancy(int spt, size_t lds, int *static_lds);
+constexpr int kBigStaticLds = 4 * 1024;  // Tables + BigShared (static LDS of k_env_big)
+constexpr int kBigAccLds = 512;          // accepted sizes held in LDS
 __global__ void k_reset(EnvParams p, const int64_t *seeds, const uint8_t *env_mask, float *obs);
 __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double *vm_mem,
                          double *cpu, double *mem, int64_t *remaining, int64_t *rank);
@@ -134,6 +137,7 @@ struct vmp_handle {
   PoisConst *pois_dev;
   uint64_t *stamps;
   uint64_t *jump_dev;
+  uint8_t *bigscr;  // k_env_big's HBM spill of the accepted / existing VM sizes
   bool big;  // k_env_big (V > 1024, or VMP_BIG_KERNEL=1)
   // eval-mode Record metrics (vmp_record.hip), allocated by vmp_record_enable
   bool rec_on;
@@ -191,6 +195,8 @@ int pw_leaves(int n) {
   return pw_leaves(n2) + pw_leaves(n - n2);
 }
 
+void carve_big(vmp_handle *h);
+
 void carve(vmp_handle *h) {
   EnvParams &p = h->prm;
   const int64_t P = h->P, V = h->V;
@@ -209,7 +215,7 @@ void carve(vmp_handle *h) {
   p.off_pm = (int32_t)off;
   off = align16(off + 16 * P);           // cpu, mem f64
   p.off_fpm = (int32_t)off;
-  off = align16(off + 12 * P);           // fcpu, fmem, fkey f32
+  off = align16(off + 8 * P);            // fcpu, fmem f32 (BF keys formed on the fly)
   p.off_thr = (int32_t)off;
   off = align16(off + 2 * P);            // tc, tm u8
   p.off_ord = (int32_t)off;
@@ -232,7 +238,67 @@ void carve(vmp_handle *h) {
   // launch): only those PM words are stored back
   p.off_pdirty = (int32_t)off;
   off = align16(off + 8 * ((2 * P + 63) / 64));
+  p.off_acc = p.off_bits + (int32_t)(2 * V);  // after the NULL list
+  p.acc_cap = (int32_t)V;
+  p.ccomp_cap = (int32_t)V;
+  p.off_ev = 0;  // k_env_big only
   p.off_pre = (int32_t)off;   // per-launch random draws follow (launch_env)
+  p.lds_wave_bytes = (int32_t)off;
+  if (h->big) carve_big(h);
+}
+
+// k_env_big's carve, sized for two workgroups per CU at P1000 / V10000 (≤ 80 KB
+// with the VM words): the regions of the action phase and of the tail share
+// one union. Heuristic side: the f32 view fcpu/fmem, thresholds tc/tm, the BF
+// tie sort's order and stacks. Tail side: the pairwise-sum LDS plan, the
+// event lists, the accepted sizes (≤ 512 in LDS) and the existing-VM sizes
+// (as many as the rest of the union holds). Steps with more accepted or
+// existing VMs than that use the handle's HBM spill (p.bigscr).
+void carve_big(vmp_handle *h) {
+  EnvParams &p = h->prm;
+  const int64_t P = h->P, V = h->V;
+  const bool deep = p.n_leaf > 1;
+  int64_t off = 0;
+  p.off_hdr = 0;
+  off = align16((int64_t)sizeof(EnvHdr));
+  p.off_pm = (int32_t)off;
+  off = align16(off + 16 * P);
+  p.off_stage = (int32_t)off;
+  off = align16(off + 8 * 16);
+  p.off_pdirty = (int32_t)off;
+  off = align16(off + 8 * ((2 * P + 63) / 64));
+  const int64_t u0 = off;
+  // heuristic side
+  p.off_fpm = (int32_t)off;
+  off = align16(off + 8 * P);  // fcpu, fmem f32 (BF keys are formed on the fly)
+  p.off_thr = (int32_t)off;
+  off = align16(off + 2 * P);
+  p.off_ord = (int32_t)off;
+  off = align16(off + 2 * P);
+  p.off_sort = (int32_t)off;
+  off = align16(off + 4 * 256 + 4 * P);
+  const int64_t heur_end = off;
+  p.off_bits = p.off_fpm;  // the wave kernel's any-fit table / NULL list: unused here
+  // tail side
+  off = u0;
+  p.off_leaf = (int32_t)off;
+  if (deep) off = align16(off + 8 * (int64_t)p.n_leaf + 4 * 192);
+  p.off_leafval = (int32_t)off;
+  if (deep) off = align16(off + 8 * (2 * (int64_t)p.n_leaf + 64));
+  p.off_ev = (int32_t)off;
+  off = align16(off + 512 * (4 + 4 + 1));
+  p.acc_cap = (int32_t)(V < kBigAccLds ? V : kBigAccLds);
+  p.off_acc = (int32_t)off;
+  off = align16(off + 2 * (int64_t)p.acc_cap);
+  p.off_ccomp = (int32_t)off;
+  int64_t cap = (heur_end - off) / 2;
+  const int64_t cap_min = V < 1024 ? V : 1024;
+  if (cap < cap_min) cap = cap_min;
+  if (cap > V) cap = V;
+  p.ccomp_cap = (int32_t)cap;
+  off = align16(off + 2 * cap);
+  if (off < heur_end) off = heur_end;
+  p.off_pre = (int32_t)off;
   p.lds_wave_bytes = (int32_t)off;
 }
 
@@ -255,20 +321,12 @@ void launch_vpt(int need, dim3 grid, dim3 block, size_t lds, hipStream_t s, cons
   else hipLaunchKernelGGL((k_env<16, ONE>), grid, block, lds, s, p, o);
 }
 
-template <bool ONE>
-void launch_big(int spt, dim3 grid, dim3 block, size_t lds, hipStream_t s, const EnvParams &p,
-                const StepOut &o) {
-  if (spt == 4) hipLaunchKernelGGL((k_env_big<4, ONE>), grid, block, lds, s, p, o);
-  else if (spt == 8) hipLaunchKernelGGL((k_env_big<8, ONE>), grid, block, lds, s, p, o);
-  else if (spt == 16) hipLaunchKernelGGL((k_env_big<16, ONE>), grid, block, lds, s, p, o);
-  else hipLaunchKernelGGL((k_env_big<20, ONE>), grid, block, lds, s, p, o);
-}
-
-// k_env_big's shape: the fewest slots per thread that fit 512 threads, and the
+// k_env_big's shape: the fewest slots per thread that fit 384 threads, and the
 // thread count (whole waves). The block's VM words live in LDS (4 B per slot).
 void big_shape(int64_t V, int &spt, int &nt) {
-  spt = V <= 4 * kBigMaxThreads ? 4 : V <= 8 * kBigMaxThreads ? 8 : V <= 16 * kBigMaxThreads ? 16 : 20;
-  nt = (int)(64 * ((V + 64 * spt - 1) / (64 * spt)));
+  int mx;
+  big_geometry(&nt, &mx);  // nt: the kernel's compile-time workgroup size (kBigNT)
+  spt = V <= 4 * nt ? 4 : V <= 8 * nt ? 8 : V <= 16 * nt ? 16 : mx;
 }
 
 int launch_env(vmp_handle *h, const StepOut &o) {
@@ -285,8 +343,7 @@ int launch_env(vmp_handle *h, const StepOut &o) {
     int spt, nt;
     big_shape(h->V, spt, nt);
     const size_t lds1 = (size_t)p.lds_wave_bytes + 4 * (size_t)spt * nt;
-    if (o.k_steps == 1) launch_big<true>(spt, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
-    else launch_big<false>(spt, dim3(h->N), dim3(nt), lds1, h->stream, p, o);
+    launch_big_env(spt, o.k_steps == 1, h->N, lds1, h->stream, p, o);
     HIP_TRY(hipGetLastError());
     return VMP_OK;
   }
@@ -325,7 +382,9 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
                vmp_handle **out) {
   if (!cfg || !out || n_env <= 0 || !seeds) return fail(VMP_EINVAL, "null argument or n_env <= 0");
   if (cfg->pms < 1 || cfg->pms > 65533) return fail(VMP_EINVAL, "pms must be in [1, 65533]");
-  if (cfg->vms < 1 || cfg->vms > kBigMaxV)
+  int big_nt, big_spt;
+  big_geometry(&big_nt, &big_spt);
+  if (cfg->vms < 1 || cfg->vms > big_nt * big_spt)
     return fail(VMP_EINVAL, "vms must be in [1, 10240] on this build");
   if (cfg->reward_function < 0 || cfg->reward_function > 2)
     return fail(VMP_EINVAL, "Function does not exist: reward_function");  // env.py:156
@@ -417,11 +476,21 @@ static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, cons
   p.pm = h->pm;
   p.hdr = h->hdr;
   carve(h);
+  if (h->big) {
+    HIP_TRY(dev_malloc(&h->bigscr, (size_t)n_env * 4 * (size_t)h->V));
+    p.bigscr = h->bigscr;
+  }
+  // diagnostic per-env clocks: -DVMP_STAMPS builds, or VMP_STAMP_BUF=1 for the
+  // workgroup timing build (-DVMP_WGTIME, tools/wgtime.py)
+  bool want_stamps = getenv("VMP_STAMP_BUF") && getenv("VMP_STAMP_BUF")[0] == '1';
 #ifdef VMP_STAMPS
-  HIP_TRY(dev_malloc(&h->stamps, sizeof(uint64_t) * kStamps * (size_t)n_env));
-  HIP_TRY(hipMemset(h->stamps, 0, sizeof(uint64_t) * kStamps * (size_t)n_env));
-  p.stamps = h->stamps;
+  want_stamps = true;
 #endif
+  if (want_stamps) {
+    HIP_TRY(dev_malloc(&h->stamps, sizeof(uint64_t) * kStamps * (size_t)n_env));
+    HIP_TRY(hipMemset(h->stamps, 0, sizeof(uint64_t) * kStamps * (size_t)n_env));
+    p.stamps = h->stamps;
+  }
   int maxn = h->V > h->P ? h->V : h->P;
   int depth = 0;
   for (int n = 0; n <= maxn; n++) depth = pw_depth(n) > depth ? pw_depth(n) : depth;
@@ -461,6 +530,7 @@ int vmp_destroy(vmp_handle *h) {
   dev_free(h->scratch_bits);
   dev_free(h->pois_dev);
   dev_free(h->jump_dev);
+  dev_free(h->bigscr);
   dev_free(h->stamps);
   vmp_record_enable(h, 0);
   delete h;
@@ -715,7 +785,9 @@ int vmp_get_counters(vmp_handle *h, int64_t *counters) {
 int vmp_get_stats(vmp_handle *h, double *stats) {
   if (!h || !stats) return fail(VMP_EINVAL, "null argument");
   if (h->V > kMaxVPT * kWaveSize)  // beyond the static per-wave buffers: the env carve
-    hipLaunchKernelGGL(k_target_means_lds, dim3(h->N), dim3(64), (size_t)h->prm.lds_wave_bytes,
+    hipLaunchKernelGGL(k_target_means_lds, dim3(h->N), dim3(64),
+                       (size_t)(align16(2 * (int64_t)h->V) + align16(8 * (int64_t)h->prm.n_leaf + 4 * 192) +
+                                8 * (2 * (int64_t)h->prm.n_leaf + 64)),
                        h->stream, h->prm);
   else
     hipLaunchKernelGGL(k_target_means, dim3((h->N + kWavesPerBlock - 1) / kWavesPerBlock),
@@ -749,6 +821,18 @@ int64_t vmp_debug_live_allocs(void) { return g_live.load(); }
 int vmp_debug_fail_alloc(int32_t n) {
   if (n < 0) return fail(VMP_EINVAL, "n must be >= 0");
   g_fail_alloc.store(n);
+  return VMP_OK;
+}
+
+int vmp_debug_occupancy(vmp_handle *h, int32_t *blocks_per_cu, int32_t *lds_bytes) {
+  if (!h || !blocks_per_cu || !lds_bytes) return fail(VMP_EINVAL, "null argument");
+  if (!h->big) return fail(VMP_EINVAL, "occupancy query covers the block kernel (V > 1024) only");
+  int spt, nt;
+  big_shape(h->V, spt, nt);
+  const size_t lds1 = (size_t)align16(h->prm.off_pre + 20 * (int64_t)kSpecDraws + 4) + 4 * (size_t)spt * nt;
+  int st = 0;
+  *blocks_per_cu = big_occupancy(spt, lds1, &st);
+  *lds_bytes = (int32_t)lds1 + st;
   return VMP_OK;
 }
 

@@ -474,8 +474,19 @@ __device__ __forceinline__ double wave_pw_sum(int n, F f, const PwLds &S) {
 // aquicksort_<float_tag> / aheapsort_ (npysort), run by ONE lane on LDS
 // arrays (index form of the pointer algorithm); stack arrays live in LDS.
 __device__ __forceinline__ bool fless(float a, float b) { return a < b || (b != b && a == a); }
+// Sort keys: an f32 array, or BestFit's fcpu[i] + fmem[i] formed at each read
+// (the same f32 sum bestfit.py:31 sorts; no key array in LDS).
+struct KeyArr {
+  const float LDSP *a;
+  __device__ __forceinline__ float operator[](int i) const { return a[i]; }
+};
+struct KeySum {
+  const float LDSP *a, *b;
+  __device__ __forceinline__ float operator[](int i) const { return a[i] + b[i]; }
+};
 
-__device__ void aheapsort_lds(const float LDSP *v, uint16_t LDSP *tosort, int n) {
+template <class KV>
+__device__ void aheapsort_lds(KV v, uint16_t LDSP *tosort, int n) {
   uint16_t LDSP *a = tosort - 1;
   int i, j, l;
   uint16_t tmp;
@@ -514,7 +525,8 @@ __device__ void aheapsort_lds(const float LDSP *v, uint16_t LDSP *tosort, int n)
 // intersect [lo, hi] is dropped instead of sorted, and positions lo..hi come
 // out exactly as the full sort leaves them (a quickselect-shaped walk:
 // ~2n element visits instead of ~n log n).
-__device__ __noinline__ void aquicksort_lds(const float LDSP *v, uint16_t LDSP *t, int num,
+template <class KV>
+__device__ __noinline__ void aquicksort_lds(KV v, uint16_t LDSP *t, int num,
                                             int32_t LDSP *stack, int lo, int hi) {
   int32_t LDSP *depth = stack + 128;
   int pl = 0, pr = num - 1;
@@ -585,7 +597,8 @@ __device__ __noinline__ void aquicksort_lds(const float LDSP *v, uint16_t LDSP *
 // Stops are ranked with ballots; the lists live in `scr` (u16, 2 x n). Small
 // partitions (<= 16) get numpy's insertion sort as a stable rank sort; the
 // depth-limit heapsort stays on lane 0.
-__device__ __noinline__ void wave_aquicksort(const float LDSP *v, uint16_t LDSP *t, int num,
+template <class KV>
+__device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
                                              int32_t LDSP *stack, int lo, int hi,
                                              uint16_t LDSP *scr) {
   const int lane = threadIdx.x & 63;
@@ -725,7 +738,6 @@ struct Lds {
   EnvHdr LDSP *hdr;                  // the env's 256-B header (scalars, RNG streams)
   double LDSP *cpu, *mem;       // f64[P] PM resources (the env state)
   float LDSP *fcpu, *fmem;      // f32[P] observation view used by the heuristics
-  float LDSP *fkey;                  // BF keys fcpu + fmem
   uint8_t LDSP *tc, *tm;        // per-PM largest fitting size (hundredths), f32 semantics
   uint16_t LDSP *ord;                // BF ascending argsort, then reversed into visiting order
   uint64_t LDSP *bc, *bm;       // action phase: the any-fit table (u32 [128] at bc)
@@ -738,8 +750,11 @@ struct Lds {
   uint64_t LDSP *svcst;              // rng4 state after each speculative draw
   uint64_t LDSP *svcfb;              // rng4 state for fallback draws
   int32_t LDSP *svcinfo;             // [0] speculative count, [1] consumed
-  uint8_t LDSP *ccomp, *mcomp;  // compressed sizes of existing VMs [V]
+  uint8_t LDSP *ccomp, *mcomp;  // compressed sizes of existing VMs [ccomp_cap]
   uint64_t LDSP *pdirty;             // bit i: PM double i (cpu | memory) changed
+  uint32_t LDSP *evw;                // k_env_big event lists [512]: VM word,
+  int32_t LDSP *evt;                 //   target / value,
+  uint8_t LDSP *evok;                //   result
   PwLds pw;
   char LDSP *base;                   // the wave's LDS region
 };
@@ -753,7 +768,6 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   L.mem = L.cpu + p.P;
   L.fcpu = reinterpret_cast<float LDSP *>(base + p.off_fpm);
   L.fmem = L.fcpu + p.P;
-  L.fkey = L.fmem + p.P;
   L.tc = reinterpret_cast<uint8_t LDSP *>(base + p.off_thr);
   L.tm = L.tc + p.P;
   L.ord = reinterpret_cast<uint16_t LDSP *>(base + p.off_ord);
@@ -761,8 +775,8 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   L.bm = L.bc + 101 * p.NW;
   L.sortstk = reinterpret_cast<int32_t LDSP *>(base + p.off_sort);
   L.nulls = reinterpret_cast<uint16_t LDSP *>(base + p.off_bits);
-  L.accc = reinterpret_cast<uint8_t LDSP *>(base + p.off_bits) + 2 * p.V;
-  L.accm = L.accc + p.V;
+  L.accc = reinterpret_cast<uint8_t LDSP *>(base + p.off_acc);
+  L.accm = L.accc + p.acc_cap;
   L.jobres = reinterpret_cast<double LDSP *>(base + p.off_stage);
   L.svcinfo = reinterpret_cast<int32_t LDSP *>(base + p.off_stage + 8 * 12);
   L.svcfb = reinterpret_cast<uint64_t LDSP *>(base + p.off_stage + 8 * 14);
@@ -771,7 +785,10 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   L.arr = reinterpret_cast<int32_t LDSP *>(base + p.off_pre + 20 * p.scap);
   L.pdirty = reinterpret_cast<uint64_t LDSP *>(base + p.off_pdirty);
   L.ccomp = reinterpret_cast<uint8_t LDSP *>(base + p.off_ccomp);
-  L.mcomp = L.ccomp + p.V;
+  L.mcomp = L.ccomp + p.ccomp_cap;
+  L.evw = reinterpret_cast<uint32_t LDSP *>(base + p.off_ev);
+  L.evt = reinterpret_cast<int32_t LDSP *>(L.evw + 512);
+  L.evok = reinterpret_cast<uint8_t LDSP *>(L.evt + 512);
   L.pw.lo = reinterpret_cast<int32_t LDSP *>(base + p.off_leaf);
   L.pw.len = L.pw.lo + p.n_leaf;
   L.pw.stk = L.pw.len + p.n_leaf;
@@ -944,7 +961,6 @@ __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int k
   int above = 0, eq = 0;
   for (int i = lane; i < P; i += 64) {
     const float key = L.fcpu[i] + L.fmem[i];
-    L.fkey[i] = key;
     L.ord[i] = (uint16_t)i;
     above += key > m;
     eq += key == m;
@@ -957,9 +973,9 @@ __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int k
   const int hi = P - above - 1, lo = P - above - eq;
   wsync();
 #ifdef VMP_SERIAL_SORT
-  if (lane == 0) aquicksort_lds(L.fkey, L.ord, P, L.sortstk, lo, hi);
+  if (lane == 0) aquicksort_lds(KeySum{L.fcpu, L.fmem}, L.ord, P, L.sortstk, lo, hi);
 #else
-  wave_aquicksort(L.fkey, L.ord, P, L.sortstk, lo, hi,
+  wave_aquicksort(KeySum{L.fcpu, L.fmem}, L.ord, P, L.sortstk, lo, hi,
                   reinterpret_cast<uint16_t LDSP *>(L.sortstk + 256));
 #endif
   wsync();
@@ -1934,6 +1950,7 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, VMP_WAVES_PER_EU_ONE) void 
   env_body<VPT, true, true>(p, o);
 }
 
+#ifndef VMP_BIG_ONLY  // (-DVMP_BIG_ONLY: register experiments on k_env_big alone)
 template __global__ void k_env_ext<1>(EnvParams, StepOut);
 template __global__ void k_env_ext<2>(EnvParams, StepOut);
 template __global__ void k_env_ext<4>(EnvParams, StepOut);
@@ -1949,6 +1966,7 @@ template __global__ void k_env<8, false>(EnvParams, StepOut);
 template __global__ void k_env<8, true>(EnvParams, StepOut);
 template __global__ void k_env<16, false>(EnvParams, StepOut);
 template __global__ void k_env<16, true>(EnvParams, StepOut);
+#endif
 
 // ------------------------------------------------------------- reset -----
 // VmEnv.reset (env.py:180-226) for masked envs, one wave per env.
@@ -2128,7 +2146,19 @@ __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, ui
 #define VMP_SLOOP _Pragma("unroll 4")
 #endif
 
-constexpr int kBigMaxSPT = 20, kBigMaxWaves = 8;
+// k_env_big's workgroup: 6 waves (two workgroups per CU at 3 waves/SIMD); a
+// compile-time thread count so slot s of a thread sits at a constant LDS
+// offset s * kBigNT * 4 (immediate ds offsets, no per-slot address registers).
+// Up to kBigMaxSPT slots per thread (V <= kBigNT * kBigMaxSPT).
+#ifndef VMP_BIG_NT
+#define VMP_BIG_NT 256
+#endif
+constexpr int kBigNT = VMP_BIG_NT;
+// per-thread slot sets (bit s: slot s * kBigNT + t)
+typedef uint64_t SMask;
+#define SBIT(s) ((SMask)1 << (s))
+constexpr int kBigMaxSPT = (10240 + kBigNT - 1) / kBigNT, kBigMaxWaves = kBigNT / 64;
+static_assert(kBigNT % 64 == 0 && kBigNT <= 512 && kBigMaxSPT <= 64, "block shape");
 // k_env_big's per-step helpers (pairwise-sum jobs, reward, draws): inlined
 // (round 3: out of line, every call saved and restored the caller's live
 // registers through scratch, 224 B per lane; inlined the kernel needs 193
@@ -2143,9 +2173,6 @@ struct BigShared {
   int64_t b64[4];
   int32_t rc[kBigMaxSPT * kBigMaxWaves];  // per slot row, per wave flag counts (row_counts)
   int32_t rtot[kBigMaxWaves];             // per wave flag totals
-  uint32_t evw[512];  // event list (one slot row of the block): VM word
-  int32_t evt[512];   // event list: target / value
-  uint8_t evok[512];  // event results
   double half[20];    // big_sum_phase: the two halves of a split job j at 2j, 2j + 1
   uint32_t fmax[128]; // big_heuristic: the any-fit table of build_fitmax
 };
@@ -2153,7 +2180,7 @@ struct BigShared {
 // Rank of this thread's flag among the flagged threads of the block
 // (ascending t) and the block total. Two barriers.
 __device__ __forceinline__ int bcx_rank(bool flag, BigShared &B, int &total) {
-  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = kBigNT >> 6;
   const uint64_t m = ballot(flag);
   __syncthreads();
   if (lane == 0) B.wcnt[wid] = __popcll(m);
@@ -2171,8 +2198,8 @@ __device__ __forceinline__ int bcx_rank(bool flag, BigShared &B, int &total) {
 // Flag counts of all SPT slot rows at once (bit s of fl = slot s*NT + t):
 // B.rc[s][wave] and the block total. Two barriers for all rows.
 template <int SPT>
-__device__ __forceinline__ int row_counts(uint32_t fl, BigShared &B) {
-  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+__device__ __forceinline__ int row_counts(SMask fl, BigShared &B) {
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = kBigNT >> 6;
   __syncthreads();
   int wt = 0;
 #pragma unroll
@@ -2191,7 +2218,7 @@ __device__ __forceinline__ int row_counts(uint32_t fl, BigShared &B) {
 // Rank (ascending VM order) of slot row s of this thread in the flag set
 // counted by row_counts; `base` carries the flags of rows < s (start at 0 and
 // call for s = 0, 1, ... in order). Valid for flagged slots only.
-__device__ __forceinline__ int slot_rank(uint32_t fl, int s, const BigShared &B, int &base) {
+__device__ __forceinline__ int slot_rank(SMask fl, int s, const BigShared &B, int &base) {
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   const uint64_t m = ballot((fl >> s) & 1u);
   int pre = 0, tot = 0;
@@ -2213,7 +2240,7 @@ __device__ __forceinline__ int slot_rank(uint32_t fl, int s, const BigShared &B,
 // row s is readlane(result, s) + its position among the wave's flags.
 template <int SPT>
 __device__ __forceinline__ int row_prefix(const BigShared &B, int &rowbase) {
-  static_assert(SPT <= 32, "one lane per slot row");
+  static_assert(SPT <= 64, "one lane per slot row");
   const int lane = lane_id(), wid = threadIdx.x >> 6;
   int tot = 0, mine = 0;
   if (lane < SPT) {
@@ -2226,7 +2253,7 @@ __device__ __forceinline__ int row_prefix(const BigShared &B, int &rowbase) {
   }
   int incl = tot;
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) {
+  for (int o = 1; o < (SPT > 32 ? 64 : 32); o <<= 1) {
     const int y = __shfl_up(incl, o);
     if (lane >= o) incl += y;
   }
@@ -2235,7 +2262,7 @@ __device__ __forceinline__ int row_prefix(const BigShared &B, int &rowbase) {
 }
 
 __device__ __forceinline__ int block_sum_int(int x, BigShared &B) {
-  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = kBigNT >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
   __syncthreads();
@@ -2247,7 +2274,7 @@ __device__ __forceinline__ int block_sum_int(int x, BigShared &B) {
 }
 
 __device__ __forceinline__ int block_min_int(int x, BigShared &B) {
-  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = kBigNT >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
   __syncthreads();
@@ -2263,15 +2290,15 @@ template <int SPT>
 __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &L, const Tables &T,
                                                  BigShared &B, uint32_t LDSP *W, int policy,
                                                  int32_t *act_out, uint8_t *valid_out STAMP_PARAMS) {
-  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+  const int t = threadIdx.x, NT = kBigNT, lane = lane_id();
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P;
   const bool bf = policy == 1;
-  uint32_t pend = 0;
+  SMask pend = 0;
 VMP_SLOOP
   for (int s = 0; s < SPT; s++)
-    if (w_pl(W[s * NT + t]) == WAIT) pend |= 1u << s;
-  uint32_t won = 0, bad = 0;
+    if (w_pl(W[s * NT + t]) == WAIT) pend |= SBIT(s);
+  SMask won = 0, bad = 0;
   int64_t n_place = 0;
   if (block_sum_int(pend != 0, B) > 0) {
     for (int i = t; i < P; i += NT) {
@@ -2308,12 +2335,12 @@ VMP_SLOOP
     };
     build_m();
     STAMP(22);
-    uint32_t hit = 0;
+    SMask hit = 0;
 VMP_SLOOP
     for (int s = 0; s < SPT; s++)
       if ((pend >> s) & 1u) {
         const uint32_t w = W[s * NT + t];
-        if (M[w_cc(w)] > (uint32_t)w_cm(w)) hit |= 1u << s;
+        if (M[w_cc(w)] > (uint32_t)w_cm(w)) hit |= SBIT(s);
       }
     STAMP(17);
 #pragma unroll 1
@@ -2327,7 +2354,7 @@ VMP_SLOOP
       if (vw == 0x7fffffff) break;
 VMP_SLOOP
       for (int s = 0; s < SPT; s++)
-        if (s * NT + t <= vw) pend &= ~(1u << s);
+        if (s * NT + t <= vw) pend &= ~SBIT(s);
       hit &= pend;
       const int ws = vw / NT, wt = vw - ws * NT;
       const uint32_t ww = W[vw];
@@ -2362,9 +2389,9 @@ VMP_SLOOP
       const bool ok = B.bc[2] != 0;
       n_place += ok;
       if (t == wt) {
-        won |= 1u << ws;
+        won |= SBIT(ws);
         if (ok) W[vw] = (ww & 0xFFFF0000u) | (uint32_t)q;
-        else bad |= 1u << ws;
+        else bad |= SBIT(ws);
         if (act_out) act_out[vw] = q;
       }
       build_m();
@@ -2376,7 +2403,7 @@ VMP_SLOOP
           const uint32_t w = W[s * NT + t];
           const int c = w_cc(w), m = w_cm(w);
           if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && !(M[c] > (uint32_t)m))
-            hit &= ~(1u << s);
+            hit &= ~SBIT(s);
         }
       }
     }
@@ -2403,9 +2430,9 @@ __device__ __forceinline__ void big_external(const EnvParams &p, const Lds &L, c
                                              BigShared &B, uint32_t LDSP *W,
                                              const int32_t *act_row, uint8_t *valid_out,
                                              int64_t &n_place, int64_t &n_susp) {
-  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+  const int t = threadIdx.x, NT = kBigNT, lane = lane_id();
   const int P = p.P, WAIT = p.P;
-VMP_SLOOP
+#pragma unroll 1
   for (int s = 0; s < SPT; s++) {
     const int v = s * NT + t;
     const uint32_t wv = W[v];
@@ -2417,15 +2444,15 @@ VMP_SLOOP
     int nev = 0;
     const int r = bcx_rank(isplace || issusp, B, nev);
     if (isplace || issusp) {
-      B.evw[r] = wv;
-      B.evt[r] = tg;
+      L.evw[r] = wv;
+      L.evt[r] = tg;
     }
     __syncthreads();
     if (t < 64) {
 #pragma unroll 1
       for (int i = 0; i < nev; i++) {  // ascending VM index
-        const uint32_t ew = B.evw[i];
-        const int et = B.evt[i];
+        const uint32_t ew = L.evw[i];
+        const int et = L.evt[i];
         const int ec = w_pl(ew);
         const double vc = T.cent[w_cc(ew)], vm = T.cent[w_cm(ew)];
         const int q = (ec == WAIT) ? et : ec;
@@ -2446,14 +2473,14 @@ VMP_SLOOP
           L.cpu[q] = cq;
           L.mem[q] = mq;
           mark_pm(L, P, q);
-          B.evok[i] = (uint8_t)eok;
+          L.evok[i] = (uint8_t)eok;
         }
         wsync();
       }
     }
     __syncthreads();
     bool ok = (tg == c) || issusp;
-    if (isplace) ok = B.evok[r] != 0;
+    if (isplace) ok = L.evok[r] != 0;
     n_place += block_sum_int(isplace && ok, B);
     n_susp += block_sum_int(issusp, B);
     if (ok && tg != c && in) W[v] = (wv & 0xFFFF0000u) | (uint32_t)tg;
@@ -2477,16 +2504,24 @@ constexpr int kBigPwDepth = VMP_BIG_PW_DEPTH;  // register plan up to n = 7688 (
 constexpr bool kBigSplitA = VMP_BIG_SPLIT_A;   // split phase A's long sums too
 // Job j over elements [o, o + m) of its source (the whole job: o = 0, m = n),
 // result to *dst.
+// spill: bit 0 the accepted sizes (jobs 0, 1), bit 1 the existing-VM sizes
+// (jobs 2, 3, 8, 9) are in the env's HBM spill instead of LDS.
 __device__ VMP_BIG_CALL void big_sum_job(const EnvParams &p, const Tables &T, char LDSP *base,
-                                         int j, int n_ex, int o, int m, double LDSP *dst) {
+                                         int j, int n_ex, int o, int m, double LDSP *dst,
+                                         uint32_t spill) {
   const Lds L = make_lds(p, base);
   const int P = p.P;
   double LDSP *res = L.jobres;
   const double *cent = T.cent;
+  // job j's u8 source in the spill: accc | accm | ccomp | mcomp, V bytes each
+  const int part = j < 2 ? j : 2 + (j & 1);
+  const bool g = (spill >> (j < 2 ? 0 : 1)) & 1u;
+  const uint8_t GLBP *gsrc = gptr(p.bigscr) + ((int64_t)blockIdx.x * 4 + part) * p.V + o;
   double r;
   if (j < 4) {
     const uint8_t LDSP *src = ((j == 0) ? L.accc : (j == 1) ? L.accm : ((j & 1) ? L.mcomp : L.ccomp)) + o;
-    r = wave_pw_sum<kBigPwDepth>(m, [=](int i) { return cent[src[i]]; }, L.pw);
+    if (g) r = wave_pw_sum<kBigPwDepth>(m, [=](int i) { return cent[gsrc[i]]; }, L.pw);
+    else r = wave_pw_sum<kBigPwDepth>(m, [=](int i) { return cent[src[i]]; }, L.pw);
   } else if (j < 8) {
     const double LDSP *src = ((j & 1) ? L.mem : L.cpu) + o;
     const double mean = j < 6 ? 0.0 : res[j - 2] / (double)P;
@@ -2499,10 +2534,16 @@ __device__ VMP_BIG_CALL void big_sum_job(const EnvParams &p, const Tables &T, ch
   } else {
     const uint8_t LDSP *src = ((j & 1) ? L.mcomp : L.ccomp) + o;
     const double mean = res[j - 6] / (double)n_ex;
-    r = wave_pw_sum<kBigPwDepth>(m, [=](int i) {
-      const double d = cent[src[i]] - mean;
-      return d * d;
-    }, L.pw);
+    if (g)
+      r = wave_pw_sum<kBigPwDepth>(m, [=](int i) {
+        const double d = cent[gsrc[i]] - mean;
+        return d * d;
+      }, L.pw);
+    else
+      r = wave_pw_sum<kBigPwDepth>(m, [=](int i) {
+        const double d = cent[src[i]] - mean;
+        return d * d;
+      }, L.pw);
   }
   wsync();
   if (lane_id() == 0) *dst = r;
@@ -2512,7 +2553,7 @@ __device__ VMP_BIG_CALL void big_sum_job(const EnvParams &p, const Tables &T, ch
 // The jobs of bit set `jobs` spread over the block's waves (all threads call
 // it; returns after a barrier). A sum past the register plan uses the LDS
 // plan, of which the carve holds one copy: those run on wave 0 in turn.
-// halves: a job with n > 128 runs as numpy's top-level split, pairwise(n) =
+// halves: a job with n > kBigSplitMin runs as numpy's top-level split, pairwise(n) =
 // pairwise(n2) + pairwise(n - n2) with n2 = n/2 - (n/2) % 8, the two halves on
 // two waves and their sum formed by wave 0 after the barrier (so only wave 0
 // may read those results).
@@ -2520,18 +2561,24 @@ __device__ __forceinline__ int big_sum_n(const EnvParams &p, int j, int k, int n
   return j < 2 ? k : (j >= 4 && j < 8) ? p.P : n_ex;
 }
 // Number of wave tasks big_sum_phase deals for `jobs`.
+// A job is split only when its halves save a pass: one wave sums 8 leaves of
+// <= 128 elements per pass (8-lane groups), so n <= 1024 takes one pass whole.
+#ifndef VMP_BIG_SPLIT_MIN
+#define VMP_BIG_SPLIT_MIN 1024
+#endif
+constexpr int kBigSplitMin = VMP_BIG_SPLIT_MIN;
 __device__ __forceinline__ int big_sum_ntask(const EnvParams &p, uint32_t jobs, int k, int n_ex,
                                              bool halves) {
   int n = 0;
-  for (; jobs; jobs &= jobs - 1) n += (halves && big_sum_n(p, __builtin_ctz(jobs), k, n_ex) > 128) ? 2 : 1;
+  for (; jobs; jobs &= jobs - 1) n += (halves && big_sum_n(p, __builtin_ctz(jobs), k, n_ex) > kBigSplitMin) ? 2 : 1;
   return n;
 }
 // block_combine: the split results are formed before a block barrier (every
 // wave may read them), else by wave 0 alone after it.
 __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &T, char LDSP *base,
                                               BigShared &B, uint32_t jobs, int k, int n_ex,
-                                              bool halves, bool block_combine) {
-  const int wid = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+                                              bool halves, bool block_combine, uint32_t spill) {
+  const int wid = threadIdx.x >> 6, nwv = kBigNT >> 6;
   double LDSP *res = reinterpret_cast<double LDSP *>(base + p.off_stage);  // L.jobres
   int slot = 0;
   uint32_t split = 0;
@@ -2540,14 +2587,14 @@ __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &
     const int j = __builtin_ctz(jobs);
     jobs &= jobs - 1;
     const int n = big_sum_n(p, j, k, n_ex);
-    const bool two = halves && n > 128;
+    const bool two = halves && n > kBigSplitMin;
     const int n2 = (n / 2) - (n / 2) % 8;
 #pragma unroll 1
     for (int h = 0; h < (two ? 2 : 1); h++) {
       const int o = two && h ? n2 : 0, m = two ? (h ? n - n2 : n2) : n;
       const int w = m > pw_reg_cap(kBigPwDepth) ? 0 : (slot++ % nwv);
       double LDSP *dst = two ? (double LDSP *)&B.half[2 * j + h] : res + j;
-      if (w == wid) big_sum_job(p, T, base, j, n_ex, o, m, dst);
+      if (w == wid) big_sum_job(p, T, base, j, n_ex, o, m, dst, spill);
     }
     if (two) split |= 1u << j;
   }
@@ -2633,15 +2680,17 @@ __device__ VMP_BIG_CALL void big_predraw(const EnvParams &p, const Tables &T, ch
 // phase is done: obs (VM part and PM part, env.py:295-296) and, with `state`,
 // the VM words and PM resources. Issued before the stats so the stores drain
 // while the pairwise sums run (the header follows at the end of the launch).
+// With `state`: the low halves (placement, sizes) of the VM words that
+// changed (the time words were written by big_tail as they changed).
 template <int SPT>
 __device__ __forceinline__ void big_store(const EnvParams &p, const Lds &L, const Tables &T,
-                                          const uint32_t LDSP *W, const uint32_t (&rem)[SPT],
-                                          uint32_t dirty, float *obs, bool state, int e) {
-  const int t = threadIdx.x, NT = blockDim.x;
+                                          const uint32_t LDSP *W, SMask dirty, float *obs,
+                                          bool state, int e) {
+  const int t = threadIdx.x, NT = kBigNT;
   const int V = p.V, P = p.P;
-  uint64_t *vmo = p.vmw + (int64_t)e * V;
-#pragma unroll
-  for (int s = 0; s < SPT; s++) {  // rem[] statically indexed
+  uint32_t *vmo = reinterpret_cast<uint32_t *>(p.vmw + (int64_t)e * V);
+VMP_SLOOP
+  for (int s = 0; s < SPT; s++) {
     const int v = s * NT + t;
     const uint32_t w = W[v];
     if (live(w)) {
@@ -2650,7 +2699,7 @@ __device__ __forceinline__ void big_store(const EnvParams &p, const Lds &L, cons
         ST_NT(obs + V + v, T.fcent[w_cc(w)]);
         ST_NT(obs + 2 * V + v, T.fcent[w_cm(w)]);
       }
-      if (state && ((dirty >> s) & 1u)) ST_NT(vmo + v, (uint64_t)w | ((uint64_t)rem[s] << 32));
+      if (state && ((dirty >> s) & 1u)) ST_NT(vmo + 2 * v, w);
     }
   }
   if (obs)
@@ -2686,29 +2735,43 @@ __device__ __forceinline__ void big_store_obs(const EnvParams &p, const Lds &L, 
 // _run_vms, _accept_vm_requests, stats + reward, termination (env_tail, block form).
 // out_obs / store_state: big_store right after the accept phase (last step of
 // the launch only).
+// The time words (high halves of the VM words: finish keys of running VMs,
+// remaining runtimes of waiting ones, §2) are read from HBM at the start of
+// each step and written back as they change (placed, suspended, finished,
+// accepted), so no per-slot time registers live across the step; the low
+// halves live in LDS (W) and are stored by big_store (`dirty`).
 template <int SPT>
 __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, const Tables &T,
-                                           BigShared &B, uint32_t LDSP *W,
-                                           uint32_t (&rem)[SPT], uint32_t run0, uint32_t &dirty,
-                                           int kstep, bool &terminated, float *out_obs,
-                                           bool store_state, bool heur, int e STAMP_PARAMS) {
-  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+                                           BigShared &B, uint32_t LDSP *W, SMask run0,
+                                           SMask &dirty, int kstep, bool &terminated,
+                                           float *out_obs, bool store_state, bool heur,
+                                           int e STAMP_PARAMS) {
+  const int t = threadIdx.x, NT = kBigNT, lane = lane_id();
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
   EnvHdr LDSP *H = L.hdr;
+  uint32_t *vw32 = reinterpret_cast<uint32_t *>(p.vmw + (int64_t)e * p.V);
   // ---- _run_vms: finish keys (env_tail), then free the finishers in ascending VM order ----
   const uint32_t t32 = (uint32_t)H->timestep;
-  uint32_t fterm = 0;
+  SMask fterm = 0;
+  {
+    uint32_t hw[SPT];  // issued together, dead after this loop
 #pragma unroll
-  for (int s = 0; s < SPT; s++) {  // rem[] statically indexed: stays in registers
-    const bool running = w_pl(W[s * NT + t]) < P;
-    if (running != (bool)((run0 >> s) & 1u)) {
-      rem[s] = running ? rem[s] + t32 : rem[s] - t32;
-      dirty |= 1u << s;
-    }
-    if (running && (int32_t)(rem[s] - t32) <= 1) {
-      fterm |= 1u << s;
-      rem[s] = 0;  // the word becomes NULL (below)
+    for (int s = 0; s < SPT; s++) hw[s] = gptr(vw32)[2 * min(s * NT + t, p.V - 1) + 1];
+#pragma unroll
+    for (int s = 0; s < SPT; s++) {
+      const int v = s * NT + t;
+      const bool running = w_pl(W[v]) < P;
+      uint32_t h = hw[s];
+      if (running != (bool)((run0 >> s) & 1u)) {
+        h = running ? h + t32 : h - t32;
+        dirty |= SBIT(s);
+      }
+      if (running && (int32_t)(h - t32) <= 1) {
+        fterm |= SBIT(s);
+        h = 0;  // the word becomes NULL (below)
+      }
+      if (h != hw[s]) ST_NT(vw32 + 2 * v + 1, h);  // padded slots never change
     }
   }
   dirty |= fterm;
@@ -2727,7 +2790,7 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
 VMP_SLOOP
       for (int s = 0; s < SPT; s++) {
         const int r = __builtin_amdgcn_readlane(pre, s) + below(ballot((fterm >> s) & 1u), lane);
-        if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) B.evw[r - j0] = W[s * NT + t];
+        if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) L.evw[r - j0] = W[s * NT + t];
       }
     }
     __syncthreads();
@@ -2735,7 +2798,7 @@ VMP_SLOOP
       const int nt = n_term - j0 < 512 ? n_term - j0 : 512;
 #pragma unroll 1
       for (int i = 0; i < nt; i++) {  // frees in ascending VM order
-        const uint32_t ew = B.evw[i];
+        const uint32_t ew = L.evw[i];
         const int q = w_pl(ew);
         double cq = L.cpu[q] - T.cent[w_cc(ew)];
         double mq = L.mem[q] - T.cent[w_cm(ew)];
@@ -2764,13 +2827,16 @@ VMP_SLOOP
       if (L.mem[i] < 1e-7) L.mem[i] = 0;
     }
   // ---- _accept_vm_requests: the first k NULL slots in VM order ----
-  uint32_t fnull = 0;
+  SMask fnull = 0;
 VMP_SLOOP
   for (int s = 0; s < SPT; s++)
-    if (w_pl(W[s * NT + t]) == NUL) fnull |= 1u << s;
+    if (w_pl(W[s * NT + t]) == NUL) fnull |= SBIT(s);
   const int n_null = row_counts<SPT>(fnull, B);
   const int64_t arrivals = L.arr[kstep];
   const int64_t k = arrivals < n_null ? arrivals : n_null;
+  // accepted sizes: LDS up to acc_cap, else the env's HBM spill (bigscr)
+  const bool acc_g = k > p.acc_cap;
+  uint8_t GLBP *gsc = gptr(p.bigscr) + (int64_t)e * 4 * p.V;
   if (k > 0) {
     Pcg r1 = ld_pcg(H, 0), r2 = ld_pcg(H, 1);
 #pragma unroll 1
@@ -2783,23 +2849,29 @@ VMP_SLOOP
           const int cm = (int)rint((p.seq_lo + p.seq_range * next_double(r2)) * 100.0);
           const uint32_t rr = svc_take(p, L);
           if (lane == 0) {
-            L.accc[j] = (uint8_t)cc;
-            L.accm[j] = (uint8_t)cm;
-            B.evt[j - j0] = (int32_t)rr;
+            if (acc_g) {
+              gsc[j] = (uint8_t)cc;
+              gsc[p.V + j] = (uint8_t)cm;
+            } else {
+              L.accc[j] = (uint8_t)cc;
+              L.accm[j] = (uint8_t)cm;
+            }
+            L.evt[j - j0] = (int32_t)rr;
           }
         }
       }
       __syncthreads();
       int rb;
       const int pre = row_prefix<SPT>(B, rb);
-#pragma unroll
-      for (int s = 0; s < SPT; s++) {  // rem[] statically indexed
+VMP_SLOOP
+      for (int s = 0; s < SPT; s++) {
         if (__builtin_amdgcn_readlane(rb, s) >= j1) break;  // later rows rank past the accepted
         const int j = __builtin_amdgcn_readlane(pre, s) + below(ballot((fnull >> s) & 1u), lane);
         if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
-          W[s * NT + t] = w_make(WAIT, L.accc[j], L.accm[j]);
-          rem[s] = (uint32_t)B.evt[j - j0];
-          dirty |= 1u << s;
+          const int cc = acc_g ? gsc[j] : L.accc[j], cm = acc_g ? gsc[p.V + j] : L.accm[j];
+          W[s * NT + t] = w_make(WAIT, cc, cm);
+          ST_NT(vw32 + 2 * (s * NT + t) + 1, (uint32_t)L.evt[j - j0]);
+          dirty |= SBIT(s);
         }
       }
       __syncthreads();
@@ -2811,33 +2883,43 @@ VMP_SLOOP
   }
   __syncthreads();
   // the VM words and PM resources are final: their owners store them now
-  if (store_state) big_store<SPT>(p, L, T, W, rem, dirty, nullptr, true, e);
+  if (store_state) big_store<SPT>(p, L, T, W, dirty, nullptr, true, e);
   STAMP(3);
   // ---- stats + reward ----
   const bool kl = p.reward == 2;
-  uint32_t fex = 0;
+  SMask fex = 0;
   int n_w = 0;
 VMP_SLOOP
   for (int s = 0; s < SPT; s++) {
     const int c = w_pl(W[s * NT + t]);
-    if (c <= WAIT) fex |= 1u << s;
+    if (c <= WAIT) fex |= SBIT(s);
     n_w += c == WAIT;
   }
   n_w = block_sum_int(n_w, B);
   const int n_ex = row_counts<SPT>(fex, B);
+  // existing-VM sizes: LDS up to ccomp_cap, else the env's HBM spill
+  const bool cc_g = n_ex > p.ccomp_cap;
   if (kl) {
     int rb;
     const int pre = row_prefix<SPT>(B, rb);
+    uint8_t LDSP *lc = L.ccomp, *lm = L.mcomp;
+    uint8_t GLBP *gc = gsc + 2 * p.V, *gm = gsc + 3 * p.V;
 VMP_SLOOP
     for (int s = 0; s < SPT; s++) {
       const int r = __builtin_amdgcn_readlane(pre, s) + below(ballot((fex >> s) & 1u), lane);
       if ((fex >> s) & 1u) {
         const uint32_t w = W[s * NT + t];
-        L.ccomp[r] = (uint8_t)w_cc(w);
-        L.mcomp[r] = (uint8_t)w_cm(w);
+        if (cc_g) {
+          gc[r] = (uint8_t)w_cc(w);
+          gm[r] = (uint8_t)w_cm(w);
+        } else {
+          lc[r] = (uint8_t)w_cc(w);
+          lm[r] = (uint8_t)w_cm(w);
+        }
       }
     }
   }
+  const uint32_t spill = (acc_g ? 1u : 0u) | (cc_g ? 2u : 0u);
   __syncthreads();
   STAMP(11);
   {  // phase A: plain sums; phase B (kl): squared deviations about their means
@@ -2850,13 +2932,13 @@ VMP_SLOOP
       if ((t >> 6) >= ws) big_store_obs(p, L, T, W, out_obs, t - 64 * ws, NT - 64 * ws);
     }
 #ifndef VMP_ABL_NOA  // timing ablations only (rewards wrong): -DVMP_ABL_NOA / -DVMP_ABL_NOB
-    if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, kBigSplitA, true);
+    if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, kBigSplitA, true, spill);
 #else
     __syncthreads();
 #endif
     STAMP(20);
 #ifndef VMP_ABL_NOB
-    if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true, false);
+    if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true, false, spill);
 #endif
     STAMP(21);
   }
@@ -2873,11 +2955,14 @@ VMP_SLOOP
 // step's registers (rem[] above all) are dead after the state store instead of
 // live around the K-step loop's back edge, which spilled them around the sums.
 template <int SPT, bool ONE>
-__global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
+#ifndef VMP_BIG_WPE_ONE  // waves/SIMD the per-step instantiation is allocated for
+#define VMP_BIG_WPE_ONE 2
+#endif
+__global__ __launch_bounds__(kBigNT, ONE ? VMP_BIG_WPE_ONE : 2) void k_env_big(EnvParams p, StepOut o) {
   extern __shared__ __align__(16) char lds[];
   __shared__ Tables T;
   __shared__ BigShared B;
-  const int t = threadIdx.x, NT = blockDim.x, lane = lane_id();
+  const int t = threadIdx.x, NT = kBigNT, lane = lane_id();
   const bool w0 = t < 64;
   const int e = blockIdx.x;
   const Lds L = make_lds(p, (char LDSP *)lds);
@@ -2887,6 +2972,9 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   __shared__ uint64_t st_lds[kStamps];
 #endif
   STAMP_DECL_AT(w0 ? (uint64_t LDSP *)st_lds : nullptr)  // thread 0's clock
+#ifdef VMP_WGTIME  // diagnostic: workgroup start / end (100 MHz) and its CU
+  const uint64_t wg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int i = t; i < 128; i += NT) {
     T.cent[i] = (double)i / 100.0;
     T.fcent[i] = (float)((double)i / 100.0);
@@ -2903,16 +2991,29 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
 #pragma unroll
   for (int j = 0; j < 4; j++) pv[j] = pm[min(j * NT + t, n_pm - 1)];
   const uint64_t GLBP *vmw = gptr(p.vmw + (int64_t)e * V);
-  uint64_t wv[SPT];
-#pragma unroll
-  for (int s = 0; s < SPT; s++) wv[s] = vmw[min(s * NT + t, V - 1)];
   __asm__ volatile("" ::: "memory");
   if (t < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[t] = hv;
-  // the random draws need only the header: wave 0 takes them while its own
-  // PM / VM loads are still in flight
-  if (o.k_steps > 0 && w0) {
-    wsync();
-    big_predraw(p, T, L.base, o.k_steps, p.jump + 4 * lane);
+  if (w0) {
+    // the random draws need only the header: wave 0 takes them while the
+    // other waves load the VM words (the two never hold registers at once)
+    if (o.k_steps > 0) {
+      wsync();
+      big_predraw(p, T, L.base, o.k_steps, p.jump + 4 * lane);
+    }
+  } else {
+    // waves 1.. load the low halves of all VM words (placement, sizes) into W;
+    // the time words are read by big_tail
+    constexpr int kLd = kBigNT - 64, kLPT = (SPT * kBigNT + kLd - 1) / kLd;
+    const int tl = t - 64;
+    const uint32_t GLBP *vw32 = reinterpret_cast<const uint32_t GLBP *>(vmw);
+    uint32_t wl[kLPT];
+#pragma unroll
+    for (int j = 0; j < kLPT; j++) wl[j] = vw32[2 * min(j * kLd + tl, V - 1)];
+#pragma unroll
+    for (int j = 0; j < kLPT; j++) {
+      const int v = j * kLd + tl;
+      if (v < SPT * kBigNT) W[v] = v < V ? wl[j] : (uint32_t)kPad;
+    }
   }
 #pragma unroll
   for (int j = 0; j < 4; j++)
@@ -2920,19 +3021,11 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
   for (int i = 4 * NT + t; i < n_pm; i += NT) L.cpu[i] = pm[i];  // P > 2 * NT
   for (int i = t; i < (n_pm + 63) / 64; i += NT) L.pdirty[i] = 0;
   for (int i = t; i < kBigMaxSPT * kBigMaxWaves; i += NT) B.rc[i] = 0;
-  uint32_t rem[SPT];
-#pragma unroll
-  for (int s = 0; s < SPT; s++) {  // rem[] statically indexed: stays in registers
-    const int v = s * NT + t;
-    const uint64_t w = v < V ? wv[s] : (uint64_t)kPad;
-    W[v] = (uint32_t)w;
-    rem[s] = (uint32_t)(w >> 32);
-  }
   __syncthreads();
   STAMP(13);
   bool term = false;
   int64_t ndone = 0;
-  uint32_t dirty = 0;  // bit s: this thread's VM word s changed (stored by big_store)
+  SMask dirty = 0;  // bit s: this thread's VM word s changed (stored by big_store)
   const int k_steps = ONE ? 1 : o.k_steps;
 #pragma unroll 1
   for (int k = 0; k < k_steps; k++) {
@@ -2940,9 +3033,9 @@ __global__ __launch_bounds__(512) void k_env_big(EnvParams p, StepOut o) {
     uint8_t *valid_row = (last && o.valid) ? o.valid + (int64_t)e * V : nullptr;
     int32_t *act_row = (last && o.act_out) ? o.act_out + (int64_t)e * V : nullptr;
     int64_t n_place = 0, n_susp = 0;
-    uint32_t run0 = 0;
+    SMask run0 = 0;
 VMP_SLOOP
-    for (int s = 0; s < SPT; s++) run0 |= (uint32_t)(w_pl(W[s * NT + t]) < P) << s;
+    for (int s = 0; s < SPT; s++) run0 |= (SMask)(w_pl(W[s * NT + t]) < P) << s;
     if (o.policy >= 0)
       n_place = big_heuristic<SPT>(p, L, T, B, W, o.policy, act_row, valid_row STAMP_ARGS);
     else
@@ -2954,7 +3047,7 @@ VMP_SLOOP
       L.hdr->suspend_action += n_susp;
     }
     __syncthreads();
-    const double r = big_tail<SPT>(p, L, T, B, W, rem, run0, dirty, k, term,
+    const double r = big_tail<SPT>(p, L, T, B, W, run0, dirty, k, term,
                                    last && o.obs ? o.obs + (int64_t)e * p.D : nullptr, last,
                                    o.policy >= 0, e
                                    STAMP_ARGS);
@@ -2972,7 +3065,7 @@ VMP_SLOOP
   __syncthreads();
   STAMP(4);
   // a stepping launch stored obs and state after its last accept phase
-  if (o.obs && o.k_steps == 0) big_store<SPT>(p, L, T, W, rem, 0u, o.obs + (int64_t)e * p.D, false, e);
+  if (o.obs && o.k_steps == 0) big_store<SPT>(p, L, T, W, 0u, o.obs + (int64_t)e * p.D, false, e);
   if (o.mask_bits) {
     uint32_t *bits = o.mask_bits + (int64_t)e * V * p.W32;
     const int A = p.A, NW32 = p.W32, WAIT = p.P, NUL = p.P + 1;
@@ -3010,15 +3103,54 @@ VMP_SLOOP
   }
   STAMP(6);
   STAMP_FLUSH();
+#ifdef VMP_WGTIME
+  __syncthreads();
+  if (t == 0 && p.stamps) {
+    uint64_t *o = p.stamps + (int64_t)e * 24;
+    o[0] = wg_t0;
+    o[1] = __builtin_amdgcn_s_memrealtime();
+    o[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    o[3] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
+#endif
 }
-template __global__ void k_env_big<4, false>(EnvParams, StepOut);
-template __global__ void k_env_big<8, false>(EnvParams, StepOut);
-template __global__ void k_env_big<16, false>(EnvParams, StepOut);
-template __global__ void k_env_big<20, false>(EnvParams, StepOut);
-template __global__ void k_env_big<4, true>(EnvParams, StepOut);
-template __global__ void k_env_big<8, true>(EnvParams, StepOut);
-template __global__ void k_env_big<16, true>(EnvParams, StepOut);
-template __global__ void k_env_big<20, true>(EnvParams, StepOut);
+template <bool ONE>
+static void launch_big_one(int spt, int n_env, size_t lds, hipStream_t s, const EnvParams &p,
+                           const StepOut &o) {
+  const dim3 grid(n_env), block(kBigNT);
+#ifndef VMP_BIG_ONLY
+  if (spt == 4) hipLaunchKernelGGL((k_env_big<4, ONE>), grid, block, lds, s, p, o);
+  else if (spt == 8) hipLaunchKernelGGL((k_env_big<8, ONE>), grid, block, lds, s, p, o);
+  else if (spt == 16) hipLaunchKernelGGL((k_env_big<16, ONE>), grid, block, lds, s, p, o);
+  else
+#endif
+  hipLaunchKernelGGL((k_env_big<kBigMaxSPT, ONE>), grid, block, lds, s, p, o);
+}
+// host side: the block kernel's geometry and launcher (vmp_capi.cpp)
+void big_geometry(int *nt, int *spt_max) {
+  *nt = kBigNT;
+  *spt_max = kBigMaxSPT;
+}
+void launch_big_env(int spt, bool one, int n_env, size_t lds, hipStream_t s, const EnvParams &p,
+                    const StepOut &o) {
+  if (one) launch_big_one<true>(spt, n_env, lds, s, p, o);
+  else launch_big_one<false>(spt, n_env, lds, s, p, o);
+}
+// workgroups per CU of the per-step block kernel at `lds` dynamic bytes, and
+// its static LDS
+int big_occupancy(int spt, size_t lds, int *static_lds) {
+  const void *f = reinterpret_cast<const void *>(&k_env_big<kBigMaxSPT, true>);
+#ifndef VMP_BIG_ONLY
+  if (spt == 4) f = reinterpret_cast<const void *>(&k_env_big<4, true>);
+  else if (spt == 8) f = reinterpret_cast<const void *>(&k_env_big<8, true>);
+  else if (spt == 16) f = reinterpret_cast<const void *>(&k_env_big<16, true>);
+#endif
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, f) == hipSuccess) *static_lds = (int)a.sharedSizeBytes;
+  int nb = -1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBigNT, lds) != hipSuccess) nb = -1;
+  return nb;
+}
 
 // _get_rank for any V: one wave per env, LDS bitmap of used PMs.
 __global__ __launch_bounds__(64) void k_rank(EnvParams p, int64_t *rank) {
@@ -3136,7 +3268,7 @@ __device__ __forceinline__ int act_obs_bf(const float LDSP *fc, const float LDSP
   }
   const int hi = P - above - 1, lo = P - above - eq;
   wsync();
-  wave_aquicksort(key, ord, P, stk, lo, hi, reinterpret_cast<uint16_t LDSP *>(stk + 256));
+  wave_aquicksort(KeyArr{key}, ord, P, stk, lo, hi, reinterpret_cast<uint16_t LDSP *>(stk + 256));
   wsync();
   for (int b = hi; b >= lo; b -= 64) {  // visiting order: descending positions
     const int pos = b - lane;

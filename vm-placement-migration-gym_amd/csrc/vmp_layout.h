@@ -75,9 +75,16 @@ struct EnvParams {
   int32_t off_leaf, off_leafval, off_stage, off_pre;
   int32_t scap;    // speculative service draws per launch
   int32_t off_pdirty;  // u64[ceil(2P/64)]: PM doubles (cpu then memory) changed this launch
+  // accepted sizes accc/accm (u8 [acc_cap] each) and the existing-VM sizes
+  // ccomp/mcomp (u8 [ccomp_cap] each); k_env_big's event lists (off_ev:
+  // u32 [512] VM words, i32 [512] targets, u8 [512] results)
+  int32_t off_acc, acc_cap, ccomp_cap, off_ev;
   // PCG64 jump table: entry j = (A, M) with state after j+1 draws = A*s + M*inc
   // (A = a^(j+1), M = sum_{i<=j} a^i mod 2^128), u64 [64][4] {A.hi, A.lo, M.hi, M.lo}
   const uint64_t *jump;
+  // k_env_big: u8 [N][4V] HBM spill of accc | accm | ccomp | mcomp for a step
+  // whose accepted (> acc_cap) or existing (> ccomp_cap) VMs exceed the LDS copy
+  uint8_t *bigscr;
 };
 
 struct StepOut {

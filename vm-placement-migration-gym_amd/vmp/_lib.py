@@ -20,7 +20,7 @@ EXPORTS = (
     "vmp_policy_head", "vmp_policy_head_backward", "vmp_policy_head_backward_bf16",
     "vmp_actor_head", "vmp_record_enable",
     "vmp_record_read",
-    "vmp_debug_fail_alloc", "vmp_debug_live_allocs", "vmp_debug_stamps",
+    "vmp_debug_fail_alloc", "vmp_debug_live_allocs", "vmp_debug_stamps", "vmp_debug_occupancy",
 )
 
 
@@ -98,6 +98,7 @@ def lib():
         "vmp_debug_fail_alloc": (ctypes.c_int, [i32]),
         "vmp_debug_live_allocs": (ctypes.c_int64, []),
         "vmp_debug_stamps": (ctypes.c_int, [P, P]),
+        "vmp_debug_occupancy": (ctypes.c_int, [P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
