@@ -36,7 +36,7 @@ for rep in range(3):
     torch.cuda.synchronize()
     s = buf.cpu().numpy()
     t0, t1 = s[:, 0] - s[:, 0].min(), s[:, 1] - s[:, 0].min()
-    hw, xcc = s[:, 2].astype(np.int64), s[:, 3].astype(np.int64)
+    hw, xcc = s[:, 5].astype(np.int64), s[:, 7].astype(np.int64)
     cu = ((hw >> 8) & 0xF) | (((hw >> 12) & 1) << 4) | (((hw >> 13) & 0x7) << 5) | ((xcc & 0xF) << 8)
     per_cu = Counter(cu.tolist())
     dur = (t1 - t0) / 100.0  # us (100 MHz)
@@ -58,6 +58,21 @@ for rep in range(3):
             r = np.corrcoef(dc[:, i], dur)[0, 1]
             print(f"   counter {i}: mean {dc[:, i].mean():.2f}, corr with duration {r:+.2f}")
     pl = dc[:, 3]  # place_action
+    # phases between the stamp points (slot = STAMP id; 0 start, 1 end)
+    seq = [(0, "start"), (13, "prologue"), (16, "heuristic"), (2, "run_vms"), (3, "accept+store"),
+           (11, "rank+compact"), (20, "stats A (+obs)"), (21, "stats B"), (12, "stats final"),
+           (4, "tail-rest"), (6, "mask/hdr"), (1, "end")]
+    prev = s[:, 0].astype(np.float64)
+    parts = []
+    for sl, nm in seq[1:]:
+        cur = s[:, sl].astype(np.float64)
+        ok = cur > 0
+        d = np.where(ok, cur - prev, 0.0) / 100.0
+        parts.append((nm, d.mean(), d[pl == 0].mean() if (pl == 0).any() else 0.0, np.corrcoef(d, pl)[0, 1] if d.std() > 0 else 0.0))
+        prev = np.where(ok, cur, prev)
+    print("   phase                mean us   (0-placement envs)  corr(placements)")
+    for nm, a, b, r in parts:
+        print(f"   {nm:20s} {a:8.2f}   {b:8.2f}   {r:+.2f}")
     for k in sorted(set(pl.tolist()))[:8]:
         m = pl == k
         print(f"   placements {k}: {m.sum()} envs, duration mean {dur[m].mean():.1f} us")

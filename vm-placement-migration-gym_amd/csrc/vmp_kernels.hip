@@ -266,6 +266,18 @@ constexpr int kStamps = 24;
     if (p.stamps && st_acc && lane_id() == 0)                                 \
       for (int _i = 0; _i < kStamps; _i++) p.stamps[(int64_t)e * kStamps + _i] += st_acc[_i]; \
   } while (0)
+#elif defined(VMP_WGTIME)
+// Workgroup timing build (k_env_big): thread 0 records the 100 MHz real-time
+// clock at every stamp point into a block LDS row; tools/wgtime.py reads it.
+__shared__ uint64_t wg_marks[24];
+#define STAMP_PARAMS
+#define STAMP_ARGS
+#define STAMP_DECL_AT(ptr)
+#define STAMP(i)                                                         \
+  do {                                                                   \
+    if (threadIdx.x == 0) wg_marks[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define STAMP_FLUSH()
 #else
 #define STAMP_PARAMS
 #define STAMP_ARGS
@@ -767,9 +779,9 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   L.cpu = reinterpret_cast<double LDSP *>(base + p.off_pm);
   L.mem = L.cpu + p.P;
   L.fcpu = reinterpret_cast<float LDSP *>(base + p.off_fpm);
-  L.fmem = L.fcpu + p.P;
+  L.fmem = L.fcpu + ((p.P + 3) & ~3);  // 16-B aligned rows (vector reads in big_choose)
   L.tc = reinterpret_cast<uint8_t LDSP *>(base + p.off_thr);
-  L.tm = L.tc + p.P;
+  L.tm = L.tc + ((p.P + 15) & ~15);
   L.ord = reinterpret_cast<uint16_t LDSP *>(base + p.off_ord);
   L.bc = reinterpret_cast<uint64_t LDSP *>(base + p.off_bits);
   L.bm = L.bc + 101 * p.NW;
@@ -2174,7 +2186,8 @@ struct BigShared {
   int32_t rc[kBigMaxSPT * kBigMaxWaves];  // per slot row, per wave flag counts (row_counts)
   int32_t rtot[kBigMaxWaves];             // per wave flag totals
   double half[20];    // big_sum_phase: the two halves of a split job j at 2j, 2j + 1
-  uint32_t fmax[128]; // big_heuristic: the any-fit table of build_fitmax
+  uint32_t fmax[kBigMaxWaves][128];  // big_heuristic: any-fit table per PM chunk
+  int32_t wmin[kBigMaxWaves];         // block_min_1b
 };
 
 // Rank of this thread's flag among the flagged threads of the block
@@ -2285,12 +2298,132 @@ __device__ __forceinline__ int block_min_int(int x, BigShared &B) {
   return s;
 }
 
+// Block-wide min with ONE barrier. Precondition: another block barrier lies
+// between two calls (the resolve loop's choose barrier), so no wave can
+// overwrite B.wmin while another still reads the previous call's values.
+__device__ __forceinline__ int block_min_1b(int x, BigShared &B) {
+  const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = kBigNT >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
+  if (lane == 0) B.wmin[wid] = x;
+  __syncthreads();
+  int s = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < nwv; i++) s = min(s, B.wmin[i]);
+  return s;
+}
+
+// PM chunk c of the block (one per wave): PMs [c*CP, min((c+1)*CP, P)).
+__device__ __forceinline__ int big_chunk_len(int P) { return (P + kBigMaxWaves - 1) / kBigMaxWaves; }
+
+// The any-fit table of PM chunk c (build_fitmax over that chunk's PMs), built
+// by the calling wave alone: the table of the whole env is the max over the
+// chunks' tables, and a placement changes one PM, so only its chunk is rebuilt.
+template <class MT>  // uint32_t * into the block's static LDS (BigShared)
+__device__ __forceinline__ void big_build_chunk(const Lds &L, MT *M, int lo, int hi) {
+  const int lane = lane_id();
+  M[lane] = 0;
+  M[lane + 64] = 0;
+  wsync();
+  for (int q = lo + lane; q < hi; q += 64) {
+    const int tcq = (int)L.tc[q];
+    if (tcq > 0) __atomic_fetch_max(&M[tcq - 1], (uint32_t)L.tm[q], __ATOMIC_RELAXED);
+  }
+  wsync();
+  const int rlo = 63 - lane, rhi = 127 - lane;
+  const bool hi_ok = rhi <= 100;
+  uint32_t c1 = hi_ok ? M[rhi] : 0u, c0 = M[rlo];
+  c1 = prefix_max32(c1);
+  c0 = max(prefix_max32(c0), (uint32_t)__builtin_amdgcn_readlane((int)c1, 63));
+  wsync();
+  M[rlo] = c0;
+  if (hi_ok) M[rhi] = c1;
+  wsync();
+}
+
+// Does some PM accept sizes (c, m): the max over the chunk tables.
+__device__ __forceinline__ bool big_anyfit(const BigShared &B, int c, int m) {
+  uint32_t x = B.fmax[0][c];
+#pragma unroll
+  for (int i = 1; i < kBigMaxWaves; i++) x = max(x, B.fmax[i][c]);
+  return x > (uint32_t)m;
+}
+
+// Wave 0's choice for sizes (kc, km): FirstFit's first fitting PM in index
+// order (firstfit.py:33-37) or BestFit's fitting PM of largest f32 key
+// (bestfit.py:33-39, ties by numpy's introsort in bf_choose). Lane l scans the
+// 16 consecutive PMs [b + 16l, b + 16l + 16) of each 1024-PM block b with
+// vector LDS reads (thresholds 16 B, f32 view 4 x 16 B per row), so a scan is
+// one round trip per block instead of one per 64 PMs. -1 if nothing fits.
+__device__ __forceinline__ int big_choose(const EnvParams &p, const Lds &L, bool bf, int kc, int km) {
+  const int lane = lane_id();
+  const int P = p.P;
+  float best = -INFINITY;
+  int cnt = 0, bi = -1, first = 0x7fffffff;
+  for (int b = 0; b < P; b += 1024) {
+    const int q0 = b + 16 * lane;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 tcw = *reinterpret_cast<const u32x4 LDSP *>(L.tc + q0);
+    const u32x4 tmw = *reinterpret_cast<const u32x4 LDSP *>(L.tm + q0);
+    f32x4 fc[4], fm[4];
+    if (bf) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        fc[j] = *reinterpret_cast<const f32x4 LDSP *>(L.fcpu + q0 + 4 * j);
+        fm[j] = *reinterpret_cast<const f32x4 LDSP *>(L.fmem + q0 + 4 * j);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const int q = q0 + j;
+      const int tcq = (int)((tcw[j >> 2] >> (8 * (j & 3))) & 0xFFu) - 1;
+      const int tmq = (int)((tmw[j >> 2] >> (8 * (j & 3))) & 0xFFu) - 1;
+      if (q < P && tcq >= kc && tmq >= km) {
+        first = min(first, q);
+        if (bf) {
+          const float key = fc[j >> 2][j & 3] + fm[j >> 2][j & 3];  // the f32 sum bestfit.py sorts
+          if (key > best) {
+            best = key;
+            cnt = 1;
+            bi = q;
+          } else if (key == best) {
+            cnt++;
+          }
+        }
+      }
+    }
+    if (!bf) {  // FirstFit: the first block with a fit decides
+      const uint64_t f = ballot(first != 0x7fffffff);
+      if (f) return __builtin_amdgcn_readlane(first, __ffsll((unsigned long long)f) - 1);
+    }
+  }
+  if (!bf) return -1;
+  float m = best;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  int tot = (best == m) ? cnt : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  if (tot == 0) return -1;
+  if (tot == 1) {
+    const uint64_t who = ballot(best == m && cnt == 1);
+    return __builtin_amdgcn_readlane(bi, __ffsll((unsigned long long)who) - 1);
+  }
+  return bf_choose(p, L, kc, km);  // tied top keys: numpy's order decides
+}
+
 // FirstFit / BestFit act fused with the action phase (heuristic_apply, block form).
+// Per step: each wave builds the f32 view, thresholds and any-fit table of its
+// PM chunk (no barrier until all are built), the pending VMs' hits are read
+// from the chunk tables, and each placement costs two block barriers: the
+// earliest winner (block_min_1b) and wave 0's choose + place + rebuild of the
+// placed PM's chunk table.
 template <int SPT>
 __device__ __forceinline__ int64_t big_heuristic(const EnvParams &p, const Lds &L, const Tables &T,
                                                  BigShared &B, uint32_t LDSP *W, int policy,
                                                  int32_t *act_out, uint8_t *valid_out STAMP_PARAMS) {
-  const int t = threadIdx.x, NT = kBigNT, lane = lane_id();
+  const int t = threadIdx.x, NT = kBigNT, lane = lane_id(), wid = t >> 6;
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P;
   const bool bf = policy == 1;
@@ -2300,112 +2433,92 @@ VMP_SLOOP
     if (w_pl(W[s * NT + t]) == WAIT) pend |= SBIT(s);
   SMask won = 0, bad = 0;
   int64_t n_place = 0;
-  if (block_sum_int(pend != 0, B) > 0) {
-    for (int i = t; i < P; i += NT) {
+  const int CP = big_chunk_len(P);
+  {  // this wave's PM chunk: f32 view, thresholds, any-fit table
+    const int lo = wid * CP, hi = min(P, lo + CP);
+    for (int i = lo + lane; i < hi; i += 64) {
       const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
       L.fcpu[i] = fcv;
       L.fmem[i] = fmv;
       L.tc[i] = (uint8_t)(fit_threshold(fcv) + 1);
       L.tm[i] = (uint8_t)(fit_threshold(fmv) + 1);
     }
-    // the any-fit table M (build_fitmax, block form) answers "does some PM
-    // accept (c, m)" for the pending VMs; only the placed PM's thresholds move,
-    // so it is rebuilt after each placement (no fit bitmaps: FirstFit's choice
-    // is a wave scan over the u8 thresholds, BestFit's is bf_choose)
-    uint32_t *M = B.fmax;
-    auto build_m = [&]() {
-      for (int i = t; i < 128; i += NT) M[i] = 0;  // NT may be 64
-      __syncthreads();
-      for (int q = t; q < P; q += NT) {
-        const int tcq = (int)L.tc[q];
-        if (tcq > 0) __atomic_fetch_max(&M[tcq - 1], (uint32_t)L.tm[q], __ATOMIC_RELAXED);
-      }
-      __syncthreads();
-      if (w0) {
-        const int rlo = 63 - lane, rhi = 127 - lane;
-        const bool hi_ok = rhi <= 100;
-        uint32_t c1 = hi_ok ? M[rhi] : 0u, c0 = M[rlo];
-        c1 = prefix_max32(c1);
-        c0 = max(prefix_max32(c0), (uint32_t)__builtin_amdgcn_readlane((int)c1, 63));
-        wsync();
-        M[rlo] = c0;
-        if (hi_ok) M[rhi] = c1;
-      }
-      __syncthreads();
-    };
-    build_m();
-    STAMP(22);
-    SMask hit = 0;
-VMP_SLOOP
-    for (int s = 0; s < SPT; s++)
-      if ((pend >> s) & 1u) {
-        const uint32_t w = W[s * NT + t];
-        if (M[w_cc(w)] > (uint32_t)w_cm(w)) hit |= SBIT(s);
-      }
-    STAMP(17);
+    wsync();
+    big_build_chunk(L, B.fmax[wid], lo, hi);
+  }
+  __syncthreads();
+  STAMP(22);
+  SMask hit = 0;
+  for (SMask r = pend; r; r &= r - 1) {
+    const int s = __builtin_ctzll(r);
+    const uint32_t w = W[s * NT + t];
+    if (big_anyfit(B, w_cc(w), w_cm(w))) hit |= SBIT(s);
+  }
+  STAMP(17);
 #pragma unroll 1
-    for (;;) {
-      // earliest VM (index order) with a fit
-      int mine = 0x7fffffff;
-VMP_SLOOP
-      for (int s = SPT - 1; s >= 0; s--)
-        if ((hit >> s) & 1u) mine = s * NT + t;
-      const int vw = block_min_int(mine, B);
-      if (vw == 0x7fffffff) break;
-VMP_SLOOP
-      for (int s = 0; s < SPT; s++)
-        if (s * NT + t <= vw) pend &= ~SBIT(s);
-      hit &= pend;
-      const int ws = vw / NT, wt = vw - ws * NT;
-      const uint32_t ww = W[vw];
-      const int kc = w_cc(ww), km = w_cm(ww);
-      STAMP(18);
-      if (w0) {
-        const int q = bf ? bf_choose(p, L, kc, km) : ff_scan(p, L, kc, km);
-        const bool ok = env_place(L, T, P, q, kc, km);
-        const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
-        wsync();
-        if (lane == 0) {
-          const float nc = L.fcpu[q] + T.fcent[kc];
-          L.fcpu[q] = nc;
-          L.tc[q] = (uint8_t)(fit_threshold(nc) + 1);
-          if (bf) {
-            const float nm = L.fmem[q] + T.fcent[km];
-            L.fmem[q] = nm;
-            L.tm[q] = (uint8_t)(fit_threshold(nm) + 1);
-          }
-          B.bc[1] = q;
-          B.bc[2] = ok;
-          B.bc[3] = tc_old;
-          B.bc[4] = (int)L.tc[q] - 1;
-          B.bc[5] = (int)L.tm[q] - 1;
-          B.bc[7] = tm_old;
+  for (;;) {
+    // earliest VM (index order) with a fit: this thread's lowest hit slot
+    const int mine = hit ? __builtin_ctzll(hit) * NT + t : 0x7fffffff;
+    const int vw = block_min_1b(mine, B);
+    if (vw == 0x7fffffff) break;
+    {  // VMs before the winner never fit again (PM loads only grow)
+      const int sm = vw >= t ? (vw - t) / NT : -1;  // slots s <= sm have s*NT + t <= vw
+      if (sm >= 0) pend &= sm >= 63 ? (SMask)0 : ~(SBIT(sm + 1) - 1);
+    }
+    hit &= pend;
+    const int ws = vw / NT, wt = vw - ws * NT;
+    const uint32_t ww = W[vw];
+    const int kc = w_cc(ww), km = w_cm(ww);
+    STAMP(18);
+    if (w0) {
+      const int q = big_choose(p, L, bf, kc, km);
+      const bool ok = env_place(L, T, P, q, kc, km);
+      const int tc_old = (int)L.tc[q] - 1, tm_old = (int)L.tm[q] - 1;
+      const float nc = L.fcpu[q] + T.fcent[kc];
+      const float nm = bf ? L.fmem[q] + T.fcent[km] : L.fmem[q];
+      const int tc_new = fit_threshold(nc), tm_new = bf ? fit_threshold(nm) : tm_old;
+      wsync();
+      if (lane == 0) {
+        L.fcpu[q] = nc;
+        L.tc[q] = (uint8_t)(tc_new + 1);
+        if (bf) {
+          L.fmem[q] = nm;
+          L.tm[q] = (uint8_t)(tm_new + 1);
         }
-        wsync();
+        B.bc[1] = q;
+        B.bc[2] = ok;
+        B.bc[3] = tc_old;
+        B.bc[4] = tc_new;
+        B.bc[5] = tm_new;
+        B.bc[7] = tm_old;
       }
-      __syncthreads();
-      STAMP(19);
-      const int q = B.bc[1];
-      const bool ok = B.bc[2] != 0;
-      n_place += ok;
-      if (t == wt) {
-        won |= SBIT(ws);
-        if (ok) W[vw] = (ww & 0xFFFF0000u) | (uint32_t)q;
-        else bad |= SBIT(ws);
-        if (act_out) act_out[vw] = q;
+      wsync();
+      if (tc_new != tc_old || tm_new != tm_old) {  // q's chunk table
+        const int c = q / CP;
+        big_build_chunk(L, B.fmax[c], c * CP, min(P, c * CP + CP));
       }
-      build_m();
-      {  // re-query the VMs q fitted before and not after
-        const int tq = B.bc[4], tc_old = B.bc[3], tmq = B.bc[5], tm_old = B.bc[7];
-VMP_SLOOP
-        for (int s = 0; s < SPT; s++) {
-          if (!((hit >> s) & 1u)) continue;
+    }
+    __syncthreads();
+    STAMP(19);
+    const int q = B.bc[1];
+    const bool ok = B.bc[2] != 0;
+    n_place += ok;
+    if (t == wt) {
+      won |= SBIT(ws);
+      if (ok) W[vw] = (ww & 0xFFFF0000u) | (uint32_t)q;
+      else bad |= SBIT(ws);
+      if (act_out) act_out[vw] = q;
+    }
+    {  // re-query the VMs q fitted before and not after
+      const int tq = B.bc[4], tc_old = B.bc[3], tmq = B.bc[5], tm_old = B.bc[7];
+      if (tq != tc_old || tmq != tm_old)
+        for (SMask r = hit; r; r &= r - 1) {
+          const int s = __builtin_ctzll(r);
           const uint32_t w = W[s * NT + t];
           const int c = w_cc(w), m = w_cm(w);
-          if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && !(M[c] > (uint32_t)m))
+          if (c <= tc_old && m <= tm_old && !(c <= tq && m <= tmq) && !big_anyfit(B, c, m))
             hit &= ~SBIT(s);
         }
-      }
     }
   }
   if (act_out || valid_out) {
@@ -2974,6 +3087,7 @@ __global__ __launch_bounds__(kBigNT, ONE ? VMP_BIG_WPE_ONE : 2) void k_env_big(E
   STAMP_DECL_AT(w0 ? (uint64_t LDSP *)st_lds : nullptr)  // thread 0's clock
 #ifdef VMP_WGTIME  // diagnostic: workgroup start / end (100 MHz) and its CU
   const uint64_t wg_t0 = __builtin_amdgcn_s_memrealtime();
+  if (t < 24) wg_marks[t] = 0;
 #endif
   for (int i = t; i < 128; i += NT) {
     T.cent[i] = (double)i / 100.0;
@@ -3106,11 +3220,13 @@ VMP_SLOOP
 #ifdef VMP_WGTIME
   __syncthreads();
   if (t == 0 && p.stamps) {
+    // slots: 0 start, 1 end, 5 HW_ID, 7 XCC_ID, else the clock at STAMP(slot)
     uint64_t *o = p.stamps + (int64_t)e * 24;
+    for (int i = 2; i < 24; i++) o[i] = wg_marks[i];
     o[0] = wg_t0;
     o[1] = __builtin_amdgcn_s_memrealtime();
-    o[2] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-    o[3] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+    o[5] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    o[7] = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
   }
 #endif
 }
