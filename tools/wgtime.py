@@ -58,8 +58,13 @@ for rep in range(3):
             r = np.corrcoef(dc[:, i], dur)[0, 1]
             print(f"   counter {i}: mean {dc[:, i].mean():.2f}, corr with duration {r:+.2f}")
     pl = dc[:, 3]  # place_action
+    ties = s[:, 23]
+    print(f"   BestFit tie sorts per env-step: mean {ties.mean():.2f} (envs with >= 1: {(ties > 0).mean():.2f}); "
+          f"duration with ties {dur[ties > 0].mean() if (ties > 0).any() else 0:.1f} us, without {dur[ties == 0].mean():.1f} us")
     # phases between the stamp points (slot = STAMP id; 0 start, 1 end)
-    seq = [(0, "start"), (13, "prologue"), (16, "heuristic"), (2, "run_vms"), (3, "accept+store"),
+    seq = [(0, "start"), (13, "prologue"), (16, "heuristic"), (8, "run: time words"),
+           (9, "run: row counts"), (10, "run: rank+frees"), (2, "run: null"), (14, "acc: null counts"),
+           (15, "acc: draw+assign"), (3, "acc: state store"),
            (11, "rank+compact"), (20, "stats A (+obs)"), (21, "stats B"), (12, "stats final"),
            (4, "tail-rest"), (6, "mask/hdr"), (1, "end")]
     prev = s[:, 0].astype(np.float64)

@@ -644,29 +644,34 @@ __device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
         t[pr - 1] = tm;
       }
       wsync();
+      // A (ascending stops in [pl+1, pr-1]) and B (stops in [pl, pr-2], kept
+      // ascending in bas: B[k] = bas[nb-1-k]) from ONE pass over [pl, pr-1]
+      // reading each key once, two 64-position batches per round trip
       uint16_t LDSP *apos = scr;
-      uint16_t LDSP *bpos = scr + (pr - pl + 1);
-      int nb = 0;  // B: descending from pr-2
-      for (int c = pr - 2; c >= pl; c -= 64) {
-        const int q = c - lane;
-        const bool f = q >= pl && !fless(vp, v[t[q]]);
-        const uint64_t m = ballot(f);
-        if (f) bpos[nb + __popcll(m & lt)] = (uint16_t)q;
-        nb += __popcll(m);
-      }
-      int na = 0;  // A: ascending from pl+1
-      for (int c = pl + 1; c <= pr - 1; c += 64) {
-        const int q = c + lane;
-        const bool f = q <= pr - 1 && !fless(v[t[q]], vp);
-        const uint64_t m = ballot(f);
-        if (f) apos[na + __popcll(m & lt)] = (uint16_t)q;
-        na += __popcll(m);
+      uint16_t LDSP *bas = scr + (pr - pl + 1);
+      int na = 0, nb = 0;
+      for (int c = pl; c <= pr - 1; c += 128) {
+        const int q0 = c + lane, q1 = c + 64 + lane;
+        const bool in0 = q0 <= pr - 1, in1 = q1 <= pr - 1;
+        const int i0 = t[in0 ? q0 : pl], i1 = t[in1 ? q1 : pl];
+        const float x0 = v[i0], x1 = v[i1];
+        const bool fa0 = in0 && q0 >= pl + 1 && !fless(x0, vp), fb0 = in0 && q0 <= pr - 2 && !fless(vp, x0);
+        const bool fa1 = in1 && q1 >= pl + 1 && !fless(x1, vp), fb1 = in1 && q1 <= pr - 2 && !fless(vp, x1);
+        const uint64_t ma0 = ballot(fa0), mb0 = ballot(fb0), ma1 = ballot(fa1), mb1 = ballot(fb1);
+        if (fa0) apos[na + __popcll(ma0 & lt)] = (uint16_t)q0;
+        if (fb0) bas[nb + __popcll(mb0 & lt)] = (uint16_t)q0;
+        na += __popcll(ma0);
+        nb += __popcll(mb0);
+        if (fa1) apos[na + __popcll(ma1 & lt)] = (uint16_t)q1;
+        if (fb1) bas[nb + __popcll(mb1 & lt)] = (uint16_t)q1;
+        na += __popcll(ma1);
+        nb += __popcll(mb1);
       }
       wsync();
       int kk = 0;  // K: A[k] < B[k] holds for a prefix of k
       for (int c = 0; c < na && c < nb; c += 64) {
         const int k = c + lane;
-        const bool sw = k < na && k < nb && (int)apos[k] < (int)bpos[k];
+        const bool sw = k < na && k < nb && (int)apos[k] < (int)bas[nb - 1 - k];
         kk += __popcll(ballot(sw));
       }
       for (int c = 0; c < kk; c += 64) {
@@ -675,7 +680,7 @@ __device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
         int qa = 0, qb = 0;
         if (k < kk) {
           qa = apos[k];
-          qb = bpos[k];
+          qb = bas[nb - 1 - k];
           xa = t[qa];
           xb = t[qb];
         }
@@ -687,7 +692,7 @@ __device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
         wsync();
       }
       int pi = apos[kk];
-      if (kk > 0 && (int)bpos[kk - 1] < pi) pi = bpos[kk - 1];
+      if (kk > 0 && (int)bas[nb - kk] < pi) pi = bas[nb - kk];
       wsync();
       if (lane == 0) {
         x = t[pi];
@@ -941,6 +946,8 @@ __device__ __forceinline__ int ff_scan(const EnvParams &p, const Lds &L, int kc,
 // keys > m, none of which fits); the scalar introsort (numpy's tie order,
 // SURVEY App. C) is run for that block only, and its highest fitting position
 // (the first in visiting order) is taken. Returns -1 if nothing fits.
+__device__ __noinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, int km, int above,
+                                   int eq);
 __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int kc, int km) {
   const int lane = lane_id();
   const int P = p.P;
@@ -973,7 +980,6 @@ __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int k
   int above = 0, eq = 0;
   for (int i = lane; i < P; i += 64) {
     const float key = L.fcpu[i] + L.fmem[i];
-    L.ord[i] = (uint16_t)i;
     above += key > m;
     eq += key == m;
   }
@@ -982,6 +988,19 @@ __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int k
     above += __shfl_xor(above, o);
     eq += __shfl_xor(eq, o);
   }
+  return bf_tie(p, L, kc, km, above, eq);
+}
+
+// BestFit's choice when eq >= 2 PMs share the largest fitting key m and
+// `above` keys exceed it (none of which fits): the tied keys occupy the
+// ascending positions [P - above - eq, P - above) of numpy's argsort; only the
+// quicksort partitions that intersect that block are sorted, and the highest
+// fitting position in it (the first in visiting order) is taken.
+__device__ __noinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, int km, int above,
+                                   int eq) {
+  const int lane = lane_id();
+  const int P = p.P;
+  for (int i = lane; i < P; i += 64) L.ord[i] = (uint16_t)i;
   const int hi = P - above - 1, lo = P - above - eq;
   wsync();
 #ifdef VMP_SERIAL_SORT
@@ -2210,9 +2229,17 @@ __device__ __forceinline__ int bcx_rank(bool flag, BigShared &B, int &total) {
 
 // Flag counts of all SPT slot rows at once (bit s of fl = slot s*NT + t):
 // B.rc[s][wave] and the block total. Two barriers for all rows.
+// With xsum: *xsum (a per-thread int) is summed over the block on the same
+// two barriers.
 template <int SPT>
-__device__ __forceinline__ int row_counts(SMask fl, BigShared &B) {
+__device__ __forceinline__ int row_counts(SMask fl, BigShared &B, int *xsum = nullptr) {
   const int lane = lane_id(), wid = threadIdx.x >> 6, nwv = kBigNT >> 6;
+  int x = 0;
+  if (xsum) {
+    x = *xsum;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  }
   __syncthreads();
   int wt = 0;
 #pragma unroll
@@ -2221,10 +2248,17 @@ __device__ __forceinline__ int row_counts(SMask fl, BigShared &B) {
     wt += c;
     if (lane == 0) B.rc[s * kBigMaxWaves + wid] = c;
   }
-  if (lane == 0) B.rtot[wid] = wt;
+  if (lane == 0) {
+    B.rtot[wid] = wt;
+    if (xsum) B.wcnt[wid] = x;
+  }
   __syncthreads();
-  int tot = 0;
-  for (int i = 0; i < nwv; i++) tot += B.rtot[i];
+  int tot = 0, xt = 0;
+  for (int i = 0; i < nwv; i++) {
+    tot += B.rtot[i];
+    if (xsum) xt += B.wcnt[i];
+  }
+  if (xsum) *xsum = xt;
   return tot;
 }
 
@@ -2360,10 +2394,11 @@ __device__ __forceinline__ int big_choose(const EnvParams &p, const Lds &L, bool
   const int P = p.P;
   float best = -INFINITY;
   int cnt = 0, bi = -1, first = 0x7fffffff;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 kfc[4], kfm[4];  // the last block's f32 view (the tie count reads it for P <= 1024)
   for (int b = 0; b < P; b += 1024) {
     const int q0 = b + 16 * lane;
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
     const u32x4 tcw = *reinterpret_cast<const u32x4 LDSP *>(L.tc + q0);
     const u32x4 tmw = *reinterpret_cast<const u32x4 LDSP *>(L.tm + q0);
     f32x4 fc[4], fm[4];
@@ -2372,6 +2407,8 @@ __device__ __forceinline__ int big_choose(const EnvParams &p, const Lds &L, bool
       for (int j = 0; j < 4; j++) {
         fc[j] = *reinterpret_cast<const f32x4 LDSP *>(L.fcpu + q0 + 4 * j);
         fm[j] = *reinterpret_cast<const f32x4 LDSP *>(L.fmem + q0 + 4 * j);
+        kfc[j] = fc[j];
+        kfm[j] = fm[j];
       }
     }
 #pragma unroll
@@ -2410,7 +2447,28 @@ __device__ __forceinline__ int big_choose(const EnvParams &p, const Lds &L, bool
     const uint64_t who = ballot(best == m && cnt == 1);
     return __builtin_amdgcn_readlane(bi, __ffsll((unsigned long long)who) - 1);
   }
-  return bf_choose(p, L, kc, km);  // tied top keys: numpy's order decides
+#ifdef VMP_WGTIME
+  if (threadIdx.x == 0) wg_marks[23] += 1;  // tie count (timing build)
+#endif
+  if (P > 1024) return bf_choose(p, L, kc, km);  // tied top keys: numpy's order decides
+  // one block: every key is still in this lane's registers
+  int above = 0, eq = 0;
+  {
+    const int q0 = 16 * lane;
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const float key = kfc[j >> 2][j & 3] + kfm[j >> 2][j & 3];
+      above += (q0 + j < P) && key > m;
+      eq += (q0 + j < P) && key == m;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    above += __shfl_xor(above, o);
+    eq += __shfl_xor(eq, o);
+  }
+  return bf_tie(p, L, kc, km, above, eq);
 }
 
 // FirstFit / BestFit act fused with the action phase (heuristic_apply, block form).
@@ -2827,6 +2885,21 @@ VMP_SLOOP
   }
 }
 
+// The state part of big_store from the owner's register copy of its VM words.
+template <int SPT>
+__device__ __forceinline__ void big_store_words(const EnvParams &p, const Lds &L,
+                                                const uint32_t (&wr)[SPT], SMask dirty, int e) {
+  const int t = threadIdx.x, NT = kBigNT;
+  const int V = p.V, P = p.P;
+  uint32_t *vmo = reinterpret_cast<uint32_t *>(p.vmw + (int64_t)e * V);
+#pragma unroll
+  for (int s = 0; s < SPT; s++)
+    if (((dirty >> s) & 1u) && live(wr[s])) ST_NT(vmo + 2 * (s * NT + t), wr[s]);
+  double *pmo = p.pm + (int64_t)e * 2 * P;
+  for (int i = t; i < 2 * P; i += NT)
+    if ((L.pdirty[i >> 6] >> (i & 63)) & 1ull) ST_NT(pmo + i, (double)L.cpu[i]);
+}
+
 // obs (env.py:295-296) from the LDS state by the threads [0, n) of a subset
 // of the block's waves (thread i of them: slots i, i + n, ...).
 __device__ __forceinline__ void big_store_obs(const EnvParams &p, const Lds &L, const Tables &T,
@@ -2867,14 +2940,19 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
   // ---- _run_vms: finish keys (env_tail), then free the finishers in ascending VM order ----
   const uint32_t t32 = (uint32_t)H->timestep;
   SMask fterm = 0;
+  // this thread's VM words, in registers for the tail's per-slot passes (the
+  // LDS copy W stays current for the cross-thread readers: frees, obs, mask)
+  uint32_t wr[SPT];
+#pragma unroll
+  for (int s = 0; s < SPT; s++) wr[s] = W[s * NT + t];
   {
-    uint32_t hw[SPT];  // issued together, dead after this loop
+    uint32_t hw[SPT];  // the time words, issued together, dead after this loop
 #pragma unroll
     for (int s = 0; s < SPT; s++) hw[s] = gptr(vw32)[2 * min(s * NT + t, p.V - 1) + 1];
 #pragma unroll
     for (int s = 0; s < SPT; s++) {
       const int v = s * NT + t;
-      const bool running = w_pl(W[v]) < P;
+      const bool running = w_pl(wr[s]) < P;
       uint32_t h = hw[s];
       if (running != (bool)((run0 >> s) & 1u)) {
         h = running ? h + t32 : h - t32;
@@ -2888,7 +2966,9 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
     }
   }
   dirty |= fterm;
+  STAMP(8);
   const int n_term = row_counts<SPT>(fterm, B);
+  STAMP(9);
   // heuristic actions never suspend, so only the PMs freed here can fall under
   // the precision clamp: they are clamped as they are freed (equal to the
   // reference's clamp after all frees: once a PM's value is < 1e-7 every
@@ -2903,7 +2983,7 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
 VMP_SLOOP
       for (int s = 0; s < SPT; s++) {
         const int r = __builtin_amdgcn_readlane(pre, s) + below(ballot((fterm >> s) & 1u), lane);
-        if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) L.evw[r - j0] = W[s * NT + t];
+        if (((fterm >> s) & 1u) && r >= j0 && r < j0 + 512) L.evw[r - j0] = wr[s];
       }
     }
     __syncthreads();
@@ -2930,9 +3010,13 @@ VMP_SLOOP
     }
     __syncthreads();
   }
-VMP_SLOOP
+  STAMP(10);
+#pragma unroll
   for (int s = 0; s < SPT; s++)
-    if ((fterm >> s) & 1u) W[s * NT + t] = w_make(NUL, 0, 0);
+    if ((fterm >> s) & 1u) {
+      wr[s] = w_make(NUL, 0, 0);
+      W[s * NT + t] = wr[s];
+    }
   STAMP(2);
   if (w0 && !clamp_inline)
     for (int i = lane; i < P; i += 64) {  // precision clamp
@@ -2941,10 +3025,11 @@ VMP_SLOOP
     }
   // ---- _accept_vm_requests: the first k NULL slots in VM order ----
   SMask fnull = 0;
-VMP_SLOOP
+#pragma unroll
   for (int s = 0; s < SPT; s++)
-    if (w_pl(W[s * NT + t]) == NUL) fnull |= SBIT(s);
+    if (w_pl(wr[s]) == NUL) fnull |= SBIT(s);
   const int n_null = row_counts<SPT>(fnull, B);
+  STAMP(14);
   const int64_t arrivals = L.arr[kstep];
   const int64_t k = arrivals < n_null ? arrivals : n_null;
   // accepted sizes: LDS up to acc_cap, else the env's HBM spill (bigscr)
@@ -2976,13 +3061,14 @@ VMP_SLOOP
       __syncthreads();
       int rb;
       const int pre = row_prefix<SPT>(B, rb);
-VMP_SLOOP
-      for (int s = 0; s < SPT; s++) {
+#pragma unroll
+      for (int s = 0; s < SPT; s++) {  // wr[] statically indexed
         if (__builtin_amdgcn_readlane(rb, s) >= j1) break;  // later rows rank past the accepted
         const int j = __builtin_amdgcn_readlane(pre, s) + below(ballot((fnull >> s) & 1u), lane);
         if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
           const int cc = acc_g ? gsc[j] : L.accc[j], cm = acc_g ? gsc[p.V + j] : L.accm[j];
-          W[s * NT + t] = w_make(WAIT, cc, cm);
+          wr[s] = w_make(WAIT, cc, cm);
+          W[s * NT + t] = wr[s];
           ST_NT(vw32 + 2 * (s * NT + t) + 1, (uint32_t)L.evt[j - j0]);
           dirty |= SBIT(s);
         }
@@ -2995,21 +3081,21 @@ VMP_SLOOP
     }
   }
   __syncthreads();
+  STAMP(15);
   // the VM words and PM resources are final: their owners store them now
-  if (store_state) big_store<SPT>(p, L, T, W, dirty, nullptr, true, e);
+  if (store_state) big_store_words<SPT>(p, L, wr, dirty, e);
   STAMP(3);
   // ---- stats + reward ----
   const bool kl = p.reward == 2;
   SMask fex = 0;
   int n_w = 0;
-VMP_SLOOP
+#pragma unroll
   for (int s = 0; s < SPT; s++) {
-    const int c = w_pl(W[s * NT + t]);
+    const int c = w_pl(wr[s]);
     if (c <= WAIT) fex |= SBIT(s);
     n_w += c == WAIT;
   }
-  n_w = block_sum_int(n_w, B);
-  const int n_ex = row_counts<SPT>(fex, B);
+  const int n_ex = row_counts<SPT>(fex, B, &n_w);
   // existing-VM sizes: LDS up to ccomp_cap, else the env's HBM spill
   const bool cc_g = n_ex > p.ccomp_cap;
   if (kl) {
@@ -3017,11 +3103,11 @@ VMP_SLOOP
     const int pre = row_prefix<SPT>(B, rb);
     uint8_t LDSP *lc = L.ccomp, *lm = L.mcomp;
     uint8_t GLBP *gc = gsc + 2 * p.V, *gm = gsc + 3 * p.V;
-VMP_SLOOP
+#pragma unroll
     for (int s = 0; s < SPT; s++) {
       const int r = __builtin_amdgcn_readlane(pre, s) + below(ballot((fex >> s) & 1u), lane);
       if ((fex >> s) & 1u) {
-        const uint32_t w = W[s * NT + t];
+        const uint32_t w = wr[s];
         if (cc_g) {
           gc[r] = (uint8_t)w_cc(w);
           gm[r] = (uint8_t)w_cm(w);
