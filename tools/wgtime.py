@@ -65,7 +65,8 @@ for rep in range(3):
     seq = [(0, "start"), (13, "prologue"), (16, "heuristic"), (8, "run: time words"),
            (9, "run: row counts"), (10, "run: rank+frees"), (2, "run: null"), (14, "acc: null counts"),
            (15, "acc: draw+assign"), (3, "acc: state store"),
-           (11, "rank+compact"), (20, "stats A (+obs)"), (21, "stats B"), (12, "stats final"),
+           (11, "rank+compact"), (17, "A: obs issue (w0)"), (18, "A: w0 sum tasks"), (20, "A: barrier"),
+           (19, "B: w0 sum tasks"), (21, "B: barrier"), (12, "stats final"),
            (4, "tail-rest"), (6, "mask/hdr"), (1, "end")]
     prev = s[:, 0].astype(np.float64)
     parts = []

@@ -2769,6 +2769,9 @@ __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &
     }
     if (two) split |= 1u << j;
   }
+#ifdef VMP_WGTIME
+  STAMP(block_combine ? 18 : 19);  // wave 0: its sum tasks of phase A / B done
+#endif
   __syncthreads();
   if (split && wid == 0) {
     if (lane_id() == 0)
@@ -2905,6 +2908,38 @@ __device__ __forceinline__ void big_store_words(const EnvParams &p, const Lds &L
 __device__ __forceinline__ void big_store_obs(const EnvParams &p, const Lds &L, const Tables &T,
                                               const uint32_t LDSP *W, float *obs, int i, int n) {
   const int V = p.V, P = p.P;
+  if (((uintptr_t)obs & 15) == 0 && (V & 3) == 0 && (P & 3) == 0) {
+    // 4 consecutive VMs / PMs per thread: one 16-B LDS read of the VM words
+    // and three 16-B streaming stores (a quarter of the store instructions)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+#pragma unroll 2
+    for (int g = i; g < V / 4; g += n) {
+      const u32x4 w = *reinterpret_cast<const u32x4 LDSP *>(W + 4 * g);
+      f32x4 pl, cc, cm;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        pl[j] = (float)w_pl(w[j]);
+        cc[j] = T.fcent[w_cc(w[j])];
+        cm[j] = T.fcent[w_cm(w[j])];
+      }
+      __builtin_nontemporal_store(pl, reinterpret_cast<f32x4 GLBP *>(gptr(obs + 4 * g)));
+      __builtin_nontemporal_store(cc, reinterpret_cast<f32x4 GLBP *>(gptr(obs + V + 4 * g)));
+      __builtin_nontemporal_store(cm, reinterpret_cast<f32x4 GLBP *>(gptr(obs + 2 * V + 4 * g)));
+    }
+    for (int g = i; g < P / 4; g += n) {
+      const f64x2 c0 = *reinterpret_cast<const f64x2 LDSP *>(L.cpu + 4 * g);
+      const f64x2 c1 = *reinterpret_cast<const f64x2 LDSP *>(L.cpu + 4 * g + 2);
+      const f64x2 m0 = *reinterpret_cast<const f64x2 LDSP *>(L.mem + 4 * g);
+      const f64x2 m1 = *reinterpret_cast<const f64x2 LDSP *>(L.mem + 4 * g + 2);
+      const f32x4 fc = {(float)c0[0], (float)c0[1], (float)c1[0], (float)c1[1]};
+      const f32x4 fm = {(float)m0[0], (float)m0[1], (float)m1[0], (float)m1[1]};
+      __builtin_nontemporal_store(fc, reinterpret_cast<f32x4 GLBP *>(gptr(obs + 3 * V + 4 * g)));
+      __builtin_nontemporal_store(fm, reinterpret_cast<f32x4 GLBP *>(gptr(obs + 3 * V + P + 4 * g)));
+    }
+    return;
+  }
 #pragma unroll 4
   for (int v = i; v < V; v += n) {
     const uint32_t w = W[v];
@@ -3130,6 +3165,9 @@ VMP_SLOOP
       const int ws = nj < nwv ? nj : 0;
       if ((t >> 6) >= ws) big_store_obs(p, L, T, W, out_obs, t - 64 * ws, NT - 64 * ws);
     }
+#ifdef VMP_WGTIME
+    STAMP(17);  // wave 0: obs issued
+#endif
 #ifndef VMP_ABL_NOA  // timing ablations only (rewards wrong): -DVMP_ABL_NOA / -DVMP_ABL_NOB
     if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, kBigSplitA, true, spill);
 #else
