@@ -275,6 +275,7 @@ def main():
         ppo_train_bf16 = _guard(bench_ppo_train, args, dev, rank, world, dist, "bf16")
         ppo_eval = _guard(bench_ppo_eval, args, dev, rank, world, dist)
     stress = None if args.no_ppo else _guard(bench_stress, args, dev, rank, world, dist)
+    stress2k = None if args.no_ppo else _guard(bench_stress, args, dev, rank, world, dist, 2048)
     out = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": K,
         "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / K, "higher_is_better": True,
@@ -305,6 +306,7 @@ def main():
         "ppo_train_bf16": ppo_train_bf16,
         "ppo_eval": ppo_eval,
         "stress_p1000_v10000": stress,
+        "stress_p1000_v10000_2048envs": stress2k,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -534,17 +536,19 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
             else "single GPU"}
 
 
-def bench_stress(args, dev, rank, world, dist):
+def bench_stress(args, dev, rank, world, dist, N=512):
     """BASELINE config 5: P1000 / V10000 at 100 % load
-    (lambda = 1000/0.55/1000), L = 1000, reward kl, BestFit act + step, 512 envs
-    per GPU on the block-per-env kernel k_env_big. Fast-forwarded 2*L = 2000
+    (lambda = 1000/0.55/1000), L = 1000, reward kl, BestFit act + step, N envs
+    per GPU (512; the 2048-env line shows the kernel at a batch that fills
+    every CU's two workgroup slots several times) on the block-per-env kernel
+    k_env_big. Fast-forwarded 2*L = 2000
     steps with the fused rollout (steady state: ~1600 running / ~380 waiting VMs
     per env), then K timed per-step launches; kernel time from HIP events on
     the launch stream."""
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
     from vmp import _lib
-    P, V, N = 1000, 10000, 512
+    P, V = 1000, 10000
     cfg = Config(pms=P, vms=V, arrival_rate=round(1000 / 0.55 / 1000, 3), service_length=1000,
                  training_steps=10000, eval_steps=100000, seed=0, reward_function="kl",
                  sequence="uniform", cap_target_util=True, beta=0.5, allow_null_action=True)
@@ -586,13 +590,13 @@ def bench_stress(args, dev, rank, world, dist):
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
             "workload": "P1000 V10000, lambda 1.818, L 1000, reward kl, BestFit act + step "
-                        "(k_env_big, one workgroup per env)", "envs_per_gpu": N,
+                        "(k_env_big: one 256-thread workgroup per env, two per CU)", "envs_per_gpu": N,
             "ff_steps": args.stress_ff, "steps": K, "mean_running": running,
             "mean_waiting": waiting, "ms_per_step": 1e3 * el / K, "kernel_ms": kern_ms,
             "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
             "pms_written_per_env_step": pmw,
             "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "kernel": "vmp::k_env_big<20, true>"}}
+                         "frac": ach / HBM_PEAK_GBS, "kernel": "vmp::k_env_big<40, true>"}}
 
 
 def bench_external(args, env, dev, stream, dist, world, P, V):

@@ -946,7 +946,7 @@ __device__ __forceinline__ int ff_scan(const EnvParams &p, const Lds &L, int kc,
 // keys > m, none of which fits); the scalar introsort (numpy's tie order,
 // SURVEY App. C) is run for that block only, and its highest fitting position
 // (the first in visiting order) is taken. Returns -1 if nothing fits.
-__device__ __noinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, int km, int above,
+__device__ __forceinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, int km, int above,
                                    int eq);
 __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int kc, int km) {
   const int lane = lane_id();
@@ -996,7 +996,7 @@ __device__ __forceinline__ int bf_choose(const EnvParams &p, const Lds &L, int k
 // ascending positions [P - above - eq, P - above) of numpy's argsort; only the
 // quicksort partitions that intersect that block are sorted, and the highest
 // fitting position in it (the first in visiting order) is taken.
-__device__ __noinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, int km, int above,
+__device__ __forceinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, int km, int above,
                                    int eq) {
   const int lane = lane_id();
   const int P = p.P;

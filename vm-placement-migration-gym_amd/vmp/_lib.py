@@ -101,7 +101,11 @@ def lib():
         "vmp_debug_occupancy": (ctypes.c_int, [P, P, P]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)
+        if f is None and name.startswith("vmp_debug_"):
+            continue  # diagnostics an older build may lack
+        if f is None:
+            raise VmpError(f"libvmp lacks {name}")
         f.restype, f.argtypes = res, args
     if L.vmp_abi_version() != 7:
         raise VmpError("libvmp ABI mismatch")
