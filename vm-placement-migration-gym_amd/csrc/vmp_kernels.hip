@@ -1191,7 +1191,19 @@ __device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, const 
   // up to scap speculative service lengths, rng4 (env.py:289), with the state
   // after each draw for the commit
   Pcg r4 = ld_pcg(H, 3);
-  const int S = (int)(need < p.scap ? need : p.scap);
+  // a one-step launch after a step that left no NULL slot and no running VM
+  // due to finish accepts nothing (_accept_vm_requests fills NULL slots only):
+  // no service length is drawn. The hint (EnvHdr::pad, written by the
+  // previous per-step launch) only gates this speculation: a draw it wrongly
+  // skipped would come from svc_fallback, from the same stream position.
+  const uint64_t hint = H->pad;
+#ifndef VMP_NO_DRAW_HINT
+  const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 0x7FFFFFFFu) == 0 &&
+                         (uint32_t)hint > (uint32_t)H->timestep + 1u;
+#else  // A/B switch
+  const bool none_free = false && hint;
+#endif
+  const int S = none_free ? 0 : (int)(need < p.scap ? need : p.scap);
   g.base = r4.s;
   g.inc = r4.inc;
   pc.valid = false;
@@ -1871,6 +1883,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   uint32_t dirty = 0;  // bit s: this lane's VM word s changed (stored at the end)
   uint32_t fb = 0;     // ONE: bit s = slot s finishes this step if it runs
   uint32_t hiv[VPT];   // ONE: the finish keys / remaining runtimes, in flight
+  uint32_t nf = 0xFFFFFFFFu;  // ONE: smallest finish key running on (EnvHdr::pad hint)
   if (ONE && !EXT) {
     // issued before the action phase, consumed after it (latency hidden by it)
 #pragma unroll
@@ -1908,6 +1921,8 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
         const bool was_run = (run0 >> s) & 1u;
         const bool f = was_run ? (int32_t)(hiv[s] - t32) <= 1 : hiv[s] <= 1u;
         fb |= (uint32_t)f << s;
+        // the next launch's hint: smallest finish key of the VMs that run on
+        if (w_pl(wa[s]) < P && !f) nf = min(nf, was_run ? hiv[s] : hiv[s] + t32);
       }
     }
     wsync();
@@ -1959,6 +1974,21 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     double *pmo = p.pm + (int64_t)e * 2 * P;
     for (int i = lane, j = 0; i < 2 * P; i += 64, j++)
       if ((L.pdirty[j] >> lane) & 1ull) ST_NT(pmo + i, (double)L.cpu[i]);
+    {  // the next launch's draw hint (predraw): per-step launches only
+      uint64_t hint = 0;
+      if (ONE) {
+        int nn = 0;
+#pragma unroll
+        for (int s = 0; s < VPT; s++) nn += __popcll(ballot(w_pl(wa[s]) == P + 1));
+        uint32_t m = nf;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+        hint = (1ull << 63) | ((uint64_t)nn << 32) | m;
+      }
+      wsync();
+      if (lane == 0) L.hdr->pad = hint;
+      wsync();
+    }
     if (lane < 32)
       gptr(reinterpret_cast<uint64_t *>(p.hdr + e))[lane] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[lane];
   }
@@ -3336,8 +3366,8 @@ VMP_SLOOP
   if (o.k_steps > 0) {
     if (o.done && t == 0) gptr(o.done)[e] = (uint8_t)term;
     if (o.done_count && t == 0) gptr(o.done_count)[e] += ndone;
-    if (t < 32)
-      gptr(reinterpret_cast<uint64_t *>(p.hdr + e))[t] = reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
+    if (t < 32)  // (no draw hint: EnvHdr::pad = 0)
+      gptr(reinterpret_cast<uint64_t *>(p.hdr + e))[t] = t == 31 ? 0ull : reinterpret_cast<uint64_t LDSP *>(L.hdr)[t];
   }
   STAMP(6);
   STAMP_FLUSH();

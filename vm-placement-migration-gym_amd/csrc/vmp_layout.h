@@ -42,7 +42,10 @@ struct alignas(16) EnvHdr {
   int64_t timestep;
   int64_t total_requests, served, suspend_action, place_action, dropped;
   double total_cpu_req, total_mem_req, waiting_ratio, tcm, tmm;
-  int64_t pad;
+  // per-step kernels' hint for the next launch's draws (predraw): bit 63
+  // valid, bits 32..62 NULL slots after the step, bits 0..31 the smallest
+  // finish key of the VMs still running (0: no hint)
+  uint64_t pad;
 };
 static_assert(sizeof(EnvHdr) == 256, "EnvHdr must be 256 B");
 
