@@ -215,9 +215,11 @@ void carve(vmp_handle *h) {
   p.off_pm = (int32_t)off;
   off = align16(off + 16 * P);           // cpu, mem f64
   p.off_fpm = (int32_t)off;
-  off = align16(off + 8 * ((P + 3) & ~3));  // fcpu, fmem f32, 16-B aligned rows (BF keys formed on the fly)
-  p.off_thr = (int32_t)off;
-  off = align16(off + 2 * align16(P));      // tc, tm u8, 16-B aligned rows
+  off = align16(off + 12 * P);           // fcpu, fmem f32 (+ P spare: the wave kernel's
+  p.off_thr = (int32_t)off;              // measured layout; BF keys are formed on the fly)
+  off = align16(off + 2 * P);            // tc, tm u8
+  p.fmem_off = (int32_t)P;
+  p.tm_off = (int32_t)P;
   p.off_ord = (int32_t)off;
   off = align16(off + 2 * P);            // BF visiting order u16
   p.off_bits = (int32_t)off;  // any-fit table (u32[128]); after the heuristic: NULL list + accepted sizes
@@ -270,9 +272,11 @@ void carve_big(vmp_handle *h) {
   const int64_t u0 = off;
   // heuristic side
   p.off_fpm = (int32_t)off;
-  off = align16(off + 8 * ((P + 3) & ~3));  // fcpu, fmem f32 (BF keys are formed on the fly)
+  off = align16(off + 8 * ((P + 3) & ~3));  // fcpu, fmem f32, 16-B aligned rows (BF keys are formed on the fly)
   p.off_thr = (int32_t)off;
-  off = align16(off + 2 * align16(P));
+  off = align16(off + 2 * align16(P));      // tc, tm u8, 16-B aligned rows (big_choose)
+  p.fmem_off = (int32_t)((P + 3) & ~3);
+  p.tm_off = (int32_t)align16(P);
   p.off_ord = (int32_t)off;
   off = align16(off + 2 * P);
   p.off_sort = (int32_t)off;

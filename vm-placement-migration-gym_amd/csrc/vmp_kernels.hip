@@ -784,9 +784,9 @@ __device__ __forceinline__ Lds make_lds(const EnvParams &p, char LDSP *base) {
   L.cpu = reinterpret_cast<double LDSP *>(base + p.off_pm);
   L.mem = L.cpu + p.P;
   L.fcpu = reinterpret_cast<float LDSP *>(base + p.off_fpm);
-  L.fmem = L.fcpu + ((p.P + 3) & ~3);  // 16-B aligned rows (vector reads in big_choose)
+  L.fmem = L.fcpu + p.fmem_off;  // k_env_big: 16-B aligned rows (vector reads in big_choose)
   L.tc = reinterpret_cast<uint8_t LDSP *>(base + p.off_thr);
-  L.tm = L.tc + ((p.P + 15) & ~15);
+  L.tm = L.tc + p.tm_off;
   L.ord = reinterpret_cast<uint16_t LDSP *>(base + p.off_ord);
   L.bc = reinterpret_cast<uint64_t LDSP *>(base + p.off_bits);
   L.bm = L.bc + 101 * p.NW;
@@ -1883,7 +1883,8 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   uint32_t dirty = 0;  // bit s: this lane's VM word s changed (stored at the end)
   uint32_t fb = 0;     // ONE: bit s = slot s finishes this step if it runs
   uint32_t hiv[VPT];   // ONE: the finish keys / remaining runtimes, in flight
-  uint32_t nf = 0xFFFFFFFFu;  // ONE: smallest finish key running on (EnvHdr::pad hint)
+  uint32_t nf = 0u;  // ONE: smallest finish key running on (EnvHdr::pad hint; 0: unknown)
+  bool want_nf = false;
   if (ONE && !EXT) {
     // issued before the action phase, consumed after it (latency hidden by it)
 #pragma unroll
@@ -1916,13 +1917,24 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     STAMP(1);
     if (ONE) {  // the time words' last use: bit s = slot s finishes this step if it runs
       const uint32_t t32 = (uint32_t)L.hdr->timestep;
+      // the next launch's draw hint needs the smallest finish key of the VMs
+      // that run on only where the last step left no NULL slot (else nf = 0)
+      const uint64_t ph = L.hdr->pad;
+      want_nf = !((ph >> 63) && ((ph >> 32) & 1u));
+      nf = want_nf ? 0xFFFFFFFFu : 0u;
 #pragma unroll
       for (int s = 0; s < VPT; s++) {  // by the placement before the action phase
         const bool was_run = (run0 >> s) & 1u;
         const bool f = was_run ? (int32_t)(hiv[s] - t32) <= 1 : hiv[s] <= 1u;
         fb |= (uint32_t)f << s;
-        // the next launch's hint: smallest finish key of the VMs that run on
-        if (w_pl(wa[s]) < P && !f) nf = min(nf, was_run ? hiv[s] : hiv[s] + t32);
+      }
+      if (want_nf) {
+#pragma unroll
+        for (int s = 0; s < VPT; s++) {
+          const bool was_run = (run0 >> s) & 1u;
+          const bool f = (fb >> s) & 1u;
+          if (w_pl(wa[s]) < P && !f) nf = min(nf, was_run ? hiv[s] : hiv[s] + t32);
+        }
       }
     }
     wsync();
@@ -1976,13 +1988,16 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
       if ((L.pdirty[j] >> lane) & 1ull) ST_NT(pmo + i, (double)L.cpu[i]);
     {  // the next launch's draw hint (predraw): per-step launches only
       uint64_t hint = 0;
-      if (ONE) {
-        int nn = 0;
+      if (ONE) {  // (the NULL count is recorded as 0 or 1: only "none" is read)
+        bool anynull = false;
 #pragma unroll
-        for (int s = 0; s < VPT; s++) nn += __popcll(ballot(w_pl(wa[s]) == P + 1));
+        for (int s = 0; s < VPT; s++) anynull |= w_pl(wa[s]) == P + 1;
         uint32_t m = nf;
+        const bool nn = ballot(anynull) != 0;
+        if (!nn && want_nf) {
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+          for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+        }
         hint = (1ull << 63) | ((uint64_t)nn << 32) | m;
       }
       wsync();

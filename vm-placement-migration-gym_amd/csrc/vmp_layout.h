@@ -82,6 +82,7 @@ struct EnvParams {
   // ccomp/mcomp (u8 [ccomp_cap] each); k_env_big's event lists (off_ev:
   // u32 [512] VM words, i32 [512] targets, u8 [512] results)
   int32_t off_acc, acc_cap, ccomp_cap, off_ev;
+  int32_t fmem_off, tm_off;  // fmem - fcpu, tm - tc (elements): P, or 16-B aligned in k_env_big
   // PCG64 jump table: entry j = (A, M) with state after j+1 draws = A*s + M*inc
   // (A = a^(j+1), M = sum_{i<=j} a^i mod 2^128), u64 [64][4] {A.hi, A.lo, M.hi, M.lo}
   const uint64_t *jump;
