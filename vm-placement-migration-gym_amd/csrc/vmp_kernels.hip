@@ -2933,10 +2933,11 @@ VMP_SLOOP
   }
 }
 
-// The state part of big_store from the owner's register copy of its VM words.
-template <int SPT>
-__device__ __forceinline__ void big_store_words(const EnvParams &p, const Lds &L,
-                                                const uint32_t (&wr)[SPT], SMask dirty, int e) {
+// The state part of big_store from the owner's copy of its VM words (WR is a
+// register array or the LDS words W, see big_tail).
+template <int SPT, class WR>
+__device__ __forceinline__ void big_store_words(const EnvParams &p, const Lds &L, const WR &wr,
+                                                SMask dirty, int e) {
   const int t = threadIdx.x, NT = kBigNT;
   const int V = p.V, P = p.P;
   uint32_t *vmo = reinterpret_cast<uint32_t *>(p.vmw + (int64_t)e * V);
@@ -3022,9 +3023,19 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
   SMask fterm = 0;
   // this thread's VM words, in registers for the tail's per-slot passes (the
   // LDS copy W stays current for the cross-thread readers: frees, obs, mask)
+#ifdef VMP_BIG_REG_WR
   uint32_t wr[SPT];
 #pragma unroll
   for (int s = 0; s < SPT; s++) wr[s] = W[s * NT + t];
+#else  // the tail reads its words from LDS: a 40-register copy (-DVMP_BIG_REG_WR)
+       // pushed the kernel to 256 VGPRs and spilled SGPRs to scratch
+       // (~49 KB of scratch traffic each way per env-step), 2 % slower
+  struct {
+    uint32_t LDSP *W;
+    int t;
+    __device__ __forceinline__ uint32_t LDSP &operator[](int s) const { return W[s * kBigNT + t]; }
+  } wr{W, t};
+#endif
   {
     uint32_t hw[SPT];  // the time words, issued together, dead after this loop
 #pragma unroll
@@ -3095,7 +3106,9 @@ VMP_SLOOP
   for (int s = 0; s < SPT; s++)
     if ((fterm >> s) & 1u) {
       wr[s] = w_make(NUL, 0, 0);
+#ifdef VMP_BIG_REG_WR
       W[s * NT + t] = wr[s];
+#endif
     }
   STAMP(2);
   if (w0 && !clamp_inline)
@@ -3148,7 +3161,9 @@ VMP_SLOOP
         if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
           const int cc = acc_g ? gsc[j] : L.accc[j], cm = acc_g ? gsc[p.V + j] : L.accm[j];
           wr[s] = w_make(WAIT, cc, cm);
+#ifdef VMP_BIG_REG_WR
           W[s * NT + t] = wr[s];
+#endif
           ST_NT(vw32 + 2 * (s * NT + t) + 1, (uint32_t)L.evt[j - j0]);
           dirty |= SBIT(s);
         }
