@@ -226,11 +226,15 @@ def main():
     cpu = None
     if rank == 0:
         from oracle import oracle as O
-        n_chk = 2
-        r_gpu = rbuf[:, :n_chk].double().cpu().numpy()
-        ctr_gpu = env.counters()[:n_chk].cpu().numpy()
+        # one env of every phase group (env i is in group i mod G), spread over
+        # the batch, replayed through the oracle over its whole age; the last
+        # fused rollout's rewards and the final counters are compared
+        G = max(1, int(args.phase_groups))
+        chk = sorted({g + G * ((g * 977) % max(1, N // G)) for g in range(G)} & set(range(N)))
+        r_gpu = rbuf[:, chk].double().cpu().numpy()
+        ctr_gpu = env.counters()[chk].cpu().numpy()
         errs, ctr_ok = [], True
-        for i in range(n_chk):
+        for j, i in enumerate(chk):
             e = O.OracleEnv(dict(CFG, seed=int(seeds[i])))
             e.eval(False)
             e.reset(int(seeds[i]))
@@ -238,20 +242,16 @@ def main():
                 e.step(e.firstfit())
             for s in range(kr):
                 _, r, _, _ = e.step(e.firstfit())
-                errs.append(abs(r - r_gpu[s, i]))
-            ctr_ok &= bool(np.array_equal(e.counters()[0], ctr_gpu[i]))
-        parity = {"reward_mae": float(np.mean(errs)), "counters_equal": ctr_ok,
-                  "envs_checked": n_chk,
-                  "steps_checked": [steps_done - int(reset_at[i]) for i in range(n_chk)]}
+                errs.append(abs(r - r_gpu[s, j]))
+            ctr_ok &= bool(np.array_equal(e.counters()[0], ctr_gpu[j]))
+        parity = {"reward_mae": float(np.mean(errs)), "reward_max_abs_err": float(np.max(errs)),
+                  "counters_equal": ctr_ok, "envs_checked": len(chk), "env_indices": chk,
+                  "phase_groups": sorted({i % G for i in chk}),
+                  "ages_checked": [steps_done - int(reset_at[i]) for i in chk],
+                  "rewards_compared": len(errs)}
 
         if world == 1 and not args.no_cpu:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            n_cpu, warm_cpu, steps_cpu = 4 * threads, 1500, 4000
-            sec, _ = O.rollout_timed(CFG, n_cpu, 0, 4, warm_cpu, steps_cpu, 0, threads)
-            cpu = {"value": n_cpu * steps_cpu / sec, "unit": "env-steps/s", "cores": threads,
-                   "kind": "port",
-                   "sample": f"{n_cpu} envs x {steps_cpu} FirstFit act+step after {warm_cpu} "
-                             f"warm-up steps, OpenMP {threads} threads (C oracle, same config)"}
+            cpu = cpu_baseline(CFG, args.cpu_threads, "same config")
 
     bpe = step_bytes(P, V, words, pmw)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
@@ -454,14 +454,7 @@ def bench_nominal(args, dev, rank, world, dist):
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        from oracle import oracle as O
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        n_cpu, warm_cpu, steps_cpu = 4 * threads, 2000, 4000
-        sec, _ = O.rollout_timed(cfg, n_cpu, 0, 4, warm_cpu, steps_cpu, 0, threads)
-        cpu = {"value": n_cpu * steps_cpu / sec, "unit": "env-steps/s", "cores": threads,
-               "kind": "port",
-               "sample": f"{n_cpu} envs x {steps_cpu} FirstFit act+step after {warm_cpu} "
-                         f"warm-up steps, OpenMP {threads} threads (C oracle, lambda 0.182)"}
+        cpu = cpu_baseline(cfg, args.cpu_threads, "lambda 0.182")
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
             "workload": "config/100.yml with vms=1000, lambda 0.182 (100 % load), L 1000, "
                         "reward wr, FirstFit act + step, one launch per step",
@@ -473,6 +466,55 @@ def bench_nominal(args, dev, rank, world, dist):
                          "frac": ach / HBM_PEAK_GBS,
                          "kernel": "vmp::k_env<16, true> (heuristic act+step)"},
             "cpu_baseline": cpu}
+
+
+def host_cpus():
+    """The host this run sees: nproc, the affinity set, the cgroup CPU quota (in
+    cores, None when unlimited) and the CPU model string."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cores": quota,
+            "cpu_model": model}
+
+
+def cpu_baseline(cfg, threads=0, what=""):
+    """SURVEY §8(d) / BASELINE.md §4 CPU baseline: the C oracle (FirstFit act +
+    VmEnv.step, training mode as the GPU leg) over OpenMP on every core this
+    process may run on (the affinity set, capped by the cgroup's CPU quota when
+    one is set: threads beyond the quota only time-slice), 16 envs per thread,
+    warmed up 2 500 steps (the GPU window's env ages), then 3 timed passes of
+    1 000 steps (one service period each); value = the median pass, spread =
+    (max - min) / median."""
+    from oracle import oracle as O
+    host = host_cpus()
+    if not threads:
+        threads = host["affinity"]
+        if host["cgroup_quota_cores"]:
+            threads = max(1, min(threads, int(host["cgroup_quota_cores"])))
+    n_env, warm, steps, reps = 16 * threads, 2500, 1000, 3
+    secs, _ = O.rollout_timed(cfg, n_env, 0, 4, warm, steps, 0, threads, eval_mode=False,
+                              reps=reps)
+    rates = n_env * steps / secs
+    med = float(np.median(rates))
+    return {"value": med, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "repeats": [float(x) for x in rates], "spread": float((rates.max() - rates.min()) / med),
+            **host,
+            "sample": f"{n_env} envs x {steps} FirstFit act+step per pass, {reps} passes (median), "
+                      f"after {warm} warm-up steps, OpenMP {threads} threads (C oracle, {what})"}
 
 
 def _guard(fn, *a):

@@ -72,7 +72,7 @@ def lib():
             "oracle_pcg_advance_raw": (u64, [u64, u64]),
             "oracle_pw_sum": (dbl, [P, i64]), "oracle_argsort_f32": (None, [P, i64, P]),
             "oracle_rollout": (i64, [P, i32, i64, i64, i64, i32, i32, i32, P, P]),
-            "oracle_rollout_timed": (dbl, [P, i32, i64, i64, i64, i64, i32, i32, P]),
+            "oracle_rollout_timed": (None, [P, i32, i64, i64, i64, i64, i32, i32, i32, i32, P, P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -166,11 +166,14 @@ def rollout(cfg: dict, n_env, seed0, stride, steps, policy=0, eval_mode=True, th
     return rs, ctr
 
 
-def rollout_timed(cfg: dict, n_env, seed0, stride, warmup, steps, policy=0, threads=1):
-    """Warm-started timed CPU rollout (bench.py cpu_baseline). Returns
-    (seconds, reward_sum[n_env])."""
+def rollout_timed(cfg: dict, n_env, seed0, stride, warmup, steps, policy=0, threads=1,
+                  eval_mode=False, reps=1):
+    """Warm-started timed CPU rollout (bench.py cpu_baseline): `reps` timed
+    passes of `steps` steps over the same envs. Returns (seconds[reps],
+    reward_sum[reps, n_env])."""
     c = make_config(cfg)
-    rs = np.zeros(n_env)
-    sec = lib().oracle_rollout_timed(ctypes.byref(c), n_env, seed0, stride, warmup, steps,
-                                     policy, threads, _p(rs))
-    return sec, rs
+    rs = np.zeros((reps, n_env))
+    secs = np.zeros(reps)
+    lib().oracle_rollout_timed(ctypes.byref(c), n_env, seed0, stride, warmup, steps, policy,
+                               threads, int(eval_mode), reps, _p(secs), _p(rs))
+    return secs, rs

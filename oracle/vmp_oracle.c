@@ -770,11 +770,15 @@ int64_t oracle_rollout(const vmp_config *cfg, int32_t n_env, int64_t seed0, int6
  * act+step iterations per env, then `steps` timed ones (wall time of the
  * parallel region between two barriers). Returns seconds. */
 #include <omp.h>
-double oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0, int64_t stride,
-                            int64_t warmup, int64_t steps, int32_t policy, int32_t n_threads,
-                            double *reward_sum) {
+// bench.py cpu_baseline: n_env envs warmed up `warmup` steps, then `reps`
+// timed passes of `steps` act+step each (secs[r] = wall seconds of pass r).
+// Envs are dealt to threads in contiguous blocks (schedule static), each
+// thread keeping its own envs across the passes.
+void oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0, int64_t stride,
+                          int64_t warmup, int64_t steps, int32_t policy, int32_t n_threads,
+                          int32_t eval_mode, int32_t reps, double *secs, double *reward_sum) {
   oenv **envs = (oenv **)calloc(n_env, sizeof(oenv *));
-  double t0 = 0, t1 = 0;
+  double tstart = 0.0;  // shared: set by one thread per pass
 #pragma omp parallel num_threads(n_threads)
   {
     int64_t *act = (int64_t *)malloc(sizeof(int64_t) * cfg->vms);
@@ -783,7 +787,7 @@ double oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0,
       vmp_config c = *cfg;
       c.seed = seed0 + stride * (int64_t)i;
       envs[i] = oracle_create(&c);
-      oracle_set_eval(envs[i], 1);
+      oracle_set_eval(envs[i], eval_mode);
       for (int64_t s = 0; s < warmup; s++) {
         if (policy == VMP_POLICY_BESTFIT) oracle_bestfit(envs[i], act);
         else oracle_firstfit(envs[i], act);
@@ -792,27 +796,28 @@ double oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0,
         oracle_step(envs[i], act, NULL, &r, &term);
       }
     }
-#pragma omp barrier
+    for (int32_t rep = 0; rep < reps; rep++) {
 #pragma omp single
-    t0 = omp_get_wtime();
+      tstart = omp_get_wtime();  // the single's implicit barrier publishes it
 #pragma omp for schedule(static)
-    for (int32_t i = 0; i < n_env; i++) {
-      double rs = 0.0;
-      for (int64_t s = 0; s < steps; s++) {
-        if (policy == VMP_POLICY_BESTFIT) oracle_bestfit(envs[i], act);
-        else oracle_firstfit(envs[i], act);
-        double r;
-        int term;
-        oracle_step(envs[i], act, NULL, &r, &term);
-        rs += r;
+      for (int32_t i = 0; i < n_env; i++) {
+        double rs = 0.0;
+        for (int64_t s = 0; s < steps; s++) {
+          if (policy == VMP_POLICY_BESTFIT) oracle_bestfit(envs[i], act);
+          else oracle_firstfit(envs[i], act);
+          double r;
+          int term;
+          oracle_step(envs[i], act, NULL, &r, &term);
+          rs += r;
+        }
+        if (reward_sum) reward_sum[(int64_t)rep * n_env + i] = rs;
       }
-      if (reward_sum) reward_sum[i] = rs;
-    }
+      // the implicit barrier of the loop: every thread is done with this pass
 #pragma omp single
-    t1 = omp_get_wtime();
+      secs[rep] = omp_get_wtime() - tstart;
+    }
     free(act);
   }
   for (int32_t i = 0; i < n_env; i++) oracle_destroy(envs[i]);
   free(envs);
-  return t1 - t0;
 }

@@ -49,10 +49,10 @@ def _argsort(v):
 def literal_act(obs, P, V, policy):
     """firstfit.py:21-38 / bestfit.py:21-40 over one f32 observation."""
     obs = np.asarray(obs, dtype=np.float32)
-    placement = obs[:V].copy()
+    placement = obs[:V].astype(np.int64)  # convert_obs_to_dict's astype(int), utils.py:41
     vm_cpu, vm_mem = obs[V:2 * V], obs[2 * V:3 * V]
     cpu, mem = obs[3 * V:3 * V + P].copy(), obs[3 * V + P:].copy()
-    action = placement.astype(np.int64)
+    action = placement.copy()
     one = np.float32(1)
     for v in range(V):
         if placement[v] != P:
@@ -77,7 +77,11 @@ def _edit(obs, P, V, g, ties):
     for i in range(N):
         pl = o[i, :V]
         pl[g.random(V) < 0.05] = P  # stale: running / NULL slots shown as waiting
-        w = pl == P
+        # off-integer placements: astype(int) truncates, so P + 0.4 waits and
+        # p + 0.3 stays on PM p
+        frac = g.random(V) < 0.05
+        pl[frac] += np.float32(0.4)
+        w = pl.astype(np.int64) == P
         o[i, V:2 * V][w] = g.uniform(0.05, 0.6, int(w.sum())).astype(np.float32)
         o[i, 2 * V:3 * V][w] = g.uniform(0.05, 0.6, int(w.sum())).astype(np.float32)
         cpu = o[i, 3 * V:3 * V + P]
@@ -129,6 +133,25 @@ def test_act_obs_on_edited_obs_equals_literal_agent(name, policy):
                                                   np.flatnonzero(got[i] != want)[:8])
             differs += int(not np.array_equal(got[i], st[i]))
     assert differs > 0, "the edits should change the action"
+    env.close()
+
+
+def test_act_obs_large_p():
+    """P = 6000 (k_act_obs keeps the PM view in up to 160 KB of LDS): edited
+    observations against the literal agents."""
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    P, V, N = 6000, 120, 2
+    cfg = dict(pms=P, vms=V, arrival_rate=6.0, service_length=30, training_steps=10000,
+               eval_steps=100000, seed=0, reward_function="wr", allow_null_action=True)
+    env = BatchedVmEnv(Config(**cfg), N, seeds=np.arange(N) * 4, device=DEV)
+    env.rollout("firstfit", 40)
+    g = np.random.default_rng(3)
+    obs = _edit(env.obs().cpu().numpy(), P, V, g, True)
+    for policy in ("firstfit", "bestfit"):
+        got = env.heuristic_act_obs(torch.from_numpy(obs).to(DEV), policy).cpu().numpy()
+        for i in range(N):
+            assert np.array_equal(got[i], literal_act(obs[i], P, V, policy)), (policy, i)
     env.close()
 
 

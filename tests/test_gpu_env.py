@@ -284,11 +284,15 @@ def test_large_v_block_kernel_vs_oracle(policy, reward):
                 _, r, _, _ = e.step(acts[i].astype(np.int64))
                 assert r == rew[i] or abs(r - rew[i]) <= 1e-12 * max(1.0, abs(r)), (P, V, t, i)
         sd = b.state()
+        # stats() at V > 1024 derives the target means with k_target_means_lds
+        # (its own LDS carve; the wr/ut steps do not compute them)
+        stats = b.stats().cpu().numpy()
         for i, e in enumerate(orc):
             so = e.state()
             assert np.array_equal(sd["vm_placement"][i].cpu().numpy(), so[0]), (P, V)
             assert np.array_equal(sd["cpu"][i].cpu().numpy(), so[3]), (P, V)
             assert np.array_equal(b.counters()[i].cpu().numpy(), e.counters()[0]), (P, V)
+            assert np.array_equal(stats[i], e.counters()[1]), (P, V, i, stats[i], e.counters()[1])
         b.close()
 
 

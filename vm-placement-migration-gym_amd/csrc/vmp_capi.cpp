@@ -610,7 +610,8 @@ int vmp_heuristic_act_obs(vmp_handle *h, int32_t policy, const float *obs, int32
   if (policy != VMP_POLICY_FIRSTFIT && policy != VMP_POLICY_BESTFIT)
     return fail(VMP_EINVAL, "unknown policy");
   const size_t lds = 18 * (size_t)h->P + 1024;  // cpu, memory, keys, order, sort stack
-  if (lds > 65536) return fail(VMP_EINVAL, "act from observation supports P <= 3583");
+  // the whole PM view in one workgroup's LDS (gfx950: 160 KB per workgroup)
+  if (lds > (size_t)160 * 1024) return fail(VMP_EINVAL, "act from observation supports P <= 9045");
   hipLaunchKernelGGL(k_act_obs, dim3(h->N), dim3(64), lds, h->stream, h->P, h->V, policy, obs,
                      actions);
   HIP_TRY(hipGetLastError());
@@ -788,12 +789,19 @@ int vmp_get_counters(vmp_handle *h, int64_t *counters) {
 
 int vmp_get_stats(vmp_handle *h, double *stats) {
   if (!h || !stats) return fail(VMP_EINVAL, "null argument");
-  if (h->V > kMaxVPT * kWaveSize)  // beyond the static per-wave buffers: the env carve
-    hipLaunchKernelGGL(k_target_means_lds, dim3(h->N), dim3(64),
-                       (size_t)(align16(2 * (int64_t)h->V) + align16(8 * (int64_t)h->prm.n_leaf + 4 * 192) +
-                                8 * (2 * (int64_t)h->prm.n_leaf + 64)),
-                       h->stream, h->prm);
-  else
+  if (h->V > kMaxVPT * kWaveSize) {
+    // beyond the static per-wave buffers: a private carve laid out from 0 for
+    // this kernel alone (ccomp | mcomp of V bytes each, then the pairwise-sum
+    // plan); the env's own carve (carve_big) places ccomp after regions this
+    // kernel does not allocate and caps it below V
+    EnvParams q = h->prm;
+    q.off_ccomp = 0;
+    q.ccomp_cap = h->V;
+    q.off_leaf = (int32_t)align16(2 * (int64_t)h->V);
+    q.off_leafval = (int32_t)(q.off_leaf + align16(8 * (int64_t)q.n_leaf + 4 * 192));
+    const size_t lds = (size_t)q.off_leafval + 8 * (2 * (size_t)q.n_leaf + 64);
+    hipLaunchKernelGGL(k_target_means_lds, dim3(h->N), dim3(64), lds, h->stream, q);
+  } else
     hipLaunchKernelGGL(k_target_means, dim3((h->N + kWavesPerBlock - 1) / kWavesPerBlock),
                        dim3(64 * kWavesPerBlock), 0, h->stream, h->prm);
   hipLaunchKernelGGL(k_counters, dim3((h->N + 255) / 256), dim3(256), 0, h->stream, h->prm,

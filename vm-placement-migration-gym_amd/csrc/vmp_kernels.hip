@@ -3596,13 +3596,14 @@ __global__ __launch_bounds__(64) void k_act_obs(int P, int V, int policy, const 
     fm[i] = o[3 * V + P + i];
   }
   wsync();
-  const float wait = (float)P;
   for (int b = 0; b < V; b += 64) {
     const int v = b + lane;
     const float pl = v < V ? o[v] : 0.f;
     const float vc = v < V ? o[V + v] : 0.f, vm = v < V ? o[2 * V + v] : 0.f;
+    // observation[:V].astype(int) (utils.py:41) truncates before the
+    // WAIT_STATUS compare: P + 0.4 waits (C++ truncation = numpy astype(int))
     int out = (int)pl;  // action = np.copy(vm_placement)
-    uint64_t todo = ballot(v < V && pl == wait);
+    uint64_t todo = ballot(v < V && out == P);
     while (todo) {
       const int l = __ffsll((unsigned long long)todo) - 1;
       todo &= todo - 1;

@@ -129,6 +129,9 @@ class Base:
         r.rank.append(info["rank"])
 
 
+ACT_OBS_MAX_P = 9045  # vmp_heuristic_act_obs: 18 P + 1024 B of LDS <= 160 KB
+
+
 class _HeuristicAgent(Base):
     POLICY = None
 
@@ -155,7 +158,17 @@ class _HeuristicAgent(Base):
         HIP kernel (vmp_heuristic_act_obs); Base.test's fused act+step path
         (vmp_heuristic_step) acts on the env state, which is that obs."""
         b = batched_env(self.env)
-        a = b.heuristic_act_obs(observation, self.POLICY).cpu().numpy().astype(np.int64)
+        if b.P > ACT_OBS_MAX_P:
+            # k_act_obs holds the PM view in one workgroup's LDS; beyond that the
+            # env-state scan (vmp_heuristic_act) serves the env's own observation
+            import torch
+            o = torch.as_tensor(observation, dtype=torch.float32, device=b.device)
+            if not torch.equal(o.reshape(b.n_envs, b.D), b.obs()):
+                raise ValueError(f"act() on an edited observation supports P <= {ACT_OBS_MAX_P} "
+                                 f"(this env has P = {b.P}); pass the env's own observation")
+            a = b.heuristic_act(self.POLICY).cpu().numpy().astype(np.int64)
+        else:
+            a = b.heuristic_act_obs(observation, self.POLICY).cpu().numpy().astype(np.int64)
         return a[0] if b is not self.env else a
 
 

@@ -66,7 +66,7 @@ class PPOConfig:
     # ---- build options (not in the reference) ----
     value_loss_broadcast: bool = True  # ppo.py:266-270 [mb,1]-[mb] broadcast
     precision: str = "f32"             # "bf16": bf16 GEMM inputs, f32 accumulate/output
-    chunk_bytes: int = 0               # logits budget per update chunk (0: 1/8 of HBM)
+    chunk_bytes: int = 0               # logits budget per update chunk (0: from free HBM, fixed at the first update)
     seed_stride: int = 4               # env/episode reset seed spacing
 
 
@@ -627,7 +627,7 @@ class PPOTrainer:
                     ss = self._allreduce(((a_mb - mean) ** 2).sum().reshape(1).double())
                     std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
                     adv_n = (a_mb - mean) / (std + 1e-10)
-                ce = max(1, min(N, self._chunk_bytes(rew.device) // max(1, mt * VA * 4)))
+                ce = max(1, min(N, self._chunk_budget(rew.device) // max(1, mt * VA * 4)))
                 self._zero_grads(params)
                 kl_sum = torch.zeros(1, dtype=torch.float64, device=rew.device)
                 clip_n = torch.zeros(1, dtype=torch.float64, device=rew.device)
@@ -686,6 +686,20 @@ class PPOTrainer:
             stats["clipfracs"] = torch.cat(clipfracs).double().cpu().tolist()
         self.stats = stats
         return stats
+
+    def _chunk_budget(self, dev):
+        """The update's chunk budget, fixed once per trainer (the chunk count sets
+        the f32 gradient summation order, so it must not move with the free
+        memory between minibatches or runs); data parallel: the minimum over
+        ranks, so every rank chunks alike."""
+        if getattr(self, "_budget", None) is None:
+            b = self._chunk_bytes(dev)
+            if self.dist:
+                t = torch.tensor([b], dtype=torch.int64, device=dev)
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+                b = int(t.item())
+            self._budget = b
+        return self._budget
 
     def _chunk_bytes(self, dev):
         """Logits budget per update chunk: PPOConfig.chunk_bytes, or what the
