@@ -533,6 +533,39 @@ def _max_over_ranks(x, dev, dist):
     return x
 
 
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (f32 matrix = vector peak)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (spec, no sparsity)
+
+
+def mlp_flops(dims):
+    """Forward multiply-add FLOPs of a Linear stack per sample: 2 sum(in * out)."""
+    return 2.0 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+
+
+def ppo_update_flops(D, H, VA, T, E, mb_evaluated, mbs):
+    """Algorithmic FLOPs of one PPOTrainer collect + update (ppo.py:172-295)
+    from the GEMM shapes: the rollout's actor forward for T x E
+    samples; the update's critic forward of the T x E + E values; per
+    evaluated minibatch (mbs x E samples) the actor and critic forward and
+    backward (3x forward, less the first layers' unneeded input gradient).
+    Recomputation (the fused bf16 head's backward) is not counted."""
+    actor, critic = [D, H, H, VA], [D, H, H, 1]
+    fa, fc = mlp_flops(actor), mlp_flops(critic)
+    first = 2.0 * D * H
+    collect = T * E * fa
+    values = (T * E + E) * fc
+    per_sample = 3 * fa - first + 3 * fc - first
+    update = values + mb_evaluated * mbs * E * per_sample
+    return collect, update
+
+
+def mfma_roofline(flops, seconds, precision, what):
+    peak = F32_MFMA_PEAK_TFLOPS if precision == "f32" else BF16_MFMA_PEAK_TFLOPS
+    ach = flops / seconds / 1e12
+    return {"bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+            "flops": flops, "what": what}
+
+
 def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
     """BASELINE config 3 (config/100.yml, PPO from scratch, reward wr, 8192 envs per
     GPU): one untimed update, then one timed update = batch_size rollout steps of
@@ -565,9 +598,26 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
         dist.barrier()
     t2 = time.perf_counter()
     total = _max_over_ranks(t2 - t0, dev, dist)
+    upd_s = _max_over_ranks(t2 - t1, dev, dist)
     steps = world * N * tr.T
+    H = ag.config.hidden_size
+    fc, fu = ppo_update_flops(env.D, H, env.V * env.A, tr.T, N, st["minibatches"] + st["kl_breaks"],
+                              ag.config.minibatch_size)
+    fused = precision == "bf16" and ag.model.bf16_fused()
+    # the fused head's backward recomputes the last layer's logits: matrix-core
+    # work beyond the algorithmic count (what a PMC MFMA-busy pass sees)
+    recompute = ((st["minibatches"] + st["kl_breaks"]) * ag.config.minibatch_size * N
+                 * 2.0 * H * env.V * env.A) if fused else 0.0
     env.close()
     return {"value": steps / total, "unit": "env-steps/s",
+            "roofline": dict(mfma_roofline(fu, upd_s, precision,
+                                           "PPOAgent.update (all GEMMs, per GPU) / update wall time"),
+                             executed_flops=fu + recompute),
+            "collect_roofline": mfma_roofline(fc, t1 - t0, precision,
+                                              "rollout actor forward / collect wall time"),
+            "head": ("fused bf16 matrix-core actor head (vmp_actor_head_bf16_fwd/_bwd)" if fused
+                     else "f32 logits + HIP head" if precision == "f32"
+                     else "bf16 GEMM -> f32 logits + HIP head"),
             "dtype": "f32" if precision == "f32" else "bf16 GEMM inputs, f32 accumulate/params",
             "workload": "config/100.yml (P100 V300), PPO train from scratch, reward wr, "
                         "hidden 512, batch 100 / minibatch 25, 4 epochs",
@@ -747,8 +797,11 @@ def bench_ppo_eval(args, dev, rank, world, dist):
     if dist:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, dev, dist)
+    flops = N * K * mlp_flops([env.D, 512, 512, env.V * env.A])
     env.close()
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f32",
+            "roofline": mfma_roofline(flops, el, "f32",
+                                      "actor forward (Network.get_action) / replayed step wall time"),
             "workload": "config/10.yml (P10 V30), PPO eval, weights-10/ppo-wr.pt, masked, "
                         "migration_ratio 0.5, one HIP graph per batched step",
             "envs_per_gpu": N, "steps": K,

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 7
+#define VMP_ABI_VERSION 8
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -258,6 +258,32 @@ int vmp_actor_head(int32_t B, int32_t K, int32_t V, int32_t A, int32_t mode, con
                    float wait_ratio, int32_t wait_index, uint64_t seed, uint64_t offset,
                    const uint64_t *rng_counter, int32_t *action, float *logprob, float *entropy,
                    float *logits_out, float *workspace, void *hip_stream);
+
+/* Training side of the fused actor head in bf16: the update's
+ * get_action(obs, action, mask) (ppo.py:115-126, called at ppo.py:258) and its
+ * backward, for the bf16 training leg (not the parity path: the reference
+ * trains in f32). h bf16[B][K] (the actor's last hidden layer rounded to
+ * bf16), weight bf16[V*A][K], bias f32[V*A], mask_bits as vmp_policy_head
+ * (nullable), action i32[B][V] (GIVEN). Needs K % 64 == 0, A <= 128, 16-byte
+ * aligned h / weight.
+ * Forward: logprob / entropy f32[B] of the given actions; logits formed tile
+ * by tile on the bf16 matrix cores (f32 accumulate) and consumed in
+ * registers, never written. workspace: nullable, 2*B*V floats. */
+int vmp_actor_head_bf16_fwd(int32_t B, int32_t K, int32_t V, int32_t A, const uint16_t *h,
+                            const uint16_t *weight, const float *bias, const uint32_t *mask_bits,
+                            const int32_t *action, float *logprob, float *entropy,
+                            float *workspace, void *hip_stream);
+/* Backward: recomputes the logits tiles and writes
+ *   dlogits[b][ld] = bf16(d logprob/entropy loss / d logits)  (ld >= V*A)
+ * with g_logprob / g_entropy f32[B] (nullable: 0), masked entries 0, as
+ * vmp_policy_head_backward_bf16 computes from stored logits. The caller runs
+ * it over row chunks (pointers offset to the chunk) and feeds each chunk's
+ * dlogits to the dW / dh GEMMs, so no [B, V*A] tensor is ever allocated. */
+int vmp_actor_head_bf16_bwd(int32_t B, int32_t K, int32_t V, int32_t A, const uint16_t *h,
+                            const uint16_t *weight, const float *bias, const uint32_t *mask_bits,
+                            const int32_t *action, const float *g_logprob,
+                            const float *g_entropy, uint16_t *dlogits, int32_t ld,
+                            void *hip_stream);
 
 /* Eval-mode Record metrics on the device (record.py:34-134, base.py:131-148):
  * on = 1 allocates the recorder and starts it from the current state (call it

@@ -137,12 +137,13 @@ def test_act_obs_on_edited_obs_equals_literal_agent(name, policy):
 
 
 def test_act_obs_large_p():
-    """P = 6000 (k_act_obs keeps the PM view in up to 160 KB of LDS): edited
-    observations against the literal agents."""
+    """P = 4000 / V = 1100 (the block kernel's env; k_act_obs keeps the PM view
+    in up to 160 KB of LDS, 73 KB here): edited observations against the
+    literal agents."""
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
-    P, V, N = 6000, 120, 2
-    cfg = dict(pms=P, vms=V, arrival_rate=6.0, service_length=30, training_steps=10000,
+    P, V, N = 4000, 1100, 2
+    cfg = dict(pms=P, vms=V, arrival_rate=20.0, service_length=30, training_steps=10000,
                eval_steps=100000, seed=0, reward_function="wr", allow_null_action=True)
     env = BatchedVmEnv(Config(**cfg), N, seeds=np.arange(N) * 4, device=DEV)
     env.rollout("firstfit", 40)

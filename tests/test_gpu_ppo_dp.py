@@ -181,3 +181,151 @@ def test_data_parallel_trainer_two_ranks_on_gpu_equals_one_process():
     assert rel <= 1e-3, rel
     assert worst <= 5e-5, worst
     env.close()
+
+
+# ---------------------------------------------------------------------------
+# BASELINE config 4 at one GPU's full share: 32 768 envs
+# over 8 MI355X is 4 096 envs per GPU; here two gloo ranks of 2 048 envs each
+# share cuda:0 (config/100.yml, hidden 512, batch 100 / minibatch 25, 4 epochs).
+N_SHARE, SHARE_WORLD = 2048, 2
+TRACE_POS = 1 << 16  # parameter positions followed step by step
+
+
+def _flat_params(m):
+    return torch.cat([p.detach().flatten() for p in m.parameters()])
+
+
+def _install_dp_trace(ag, idx, out):
+    """After every AdamW step: the parameters at `idx`; before the first: the
+    (all-reduced, clipped) flat gradient."""
+    st = ag.optimizer.step
+
+    def step(*a, **k):
+        if "g" not in out:
+            out["g"] = torch.cat([p.grad.flatten() for p in ag.model.parameters()]).double()[
+                idx].cpu().numpy()
+        r = st(*a, **k)
+        out.setdefault("p", []).append(_flat_params(ag.model)[idx].double().cpu().numpy())
+        return r
+    ag.optimizer.step = step
+
+
+def _share_worker(rank, world, port, tmp, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        env, ag = _agent(N_SHARE)
+        p0 = _flat_params(ag.model)
+        idx = torch.randperm(p0.numel(), generator=torch.Generator().manual_seed(11))[
+            :TRACE_POS].to(p0.device)
+        tr = ag.trainer()
+        tr.collect()
+        np.savez(os.path.join(tmp, f"roll{rank}.npz"),
+                 counters=env.counters().cpu().numpy(),
+                 **{k: getattr(tr, k).cpu().numpy() for k in BUFS})
+        trace = {"p0": p0[idx].double().cpu().numpy()}
+        _install_dp_trace(ag, idx, trace)
+        st = tr.update()
+        np.savez(os.path.join(tmp, f"res{rank}.npz"), p0_full=p0.cpu().numpy(),
+                 p1_full=_flat_params(ag.model).cpu().numpy(), g=trace["g"],
+                 steps=np.stack(trace["p"]), p0=trace["p0"], idx=idx.cpu().numpy())
+        q.put((rank, int(ag.model.rng.seed), st["minibatches"], st["kl_breaks"]))
+        env.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config4_full_share_two_ranks_vs_oracle_and_one_process(tmp_path):
+    """Two ranks x 2 048 envs (one GPU's share of config 4) on the HIP path:
+      - 2 sampled envs of EACH rank replayed through the C oracle: masks,
+        observations, f32 rewards and counters bit-exact;
+      - every sampled action of both ranks valid under its mask;
+      - ranks' parameters bit-identical before and after the update;
+      - the first AdamW step's all-reduced gradient within 3e-5 relative L2 of
+        ONE process holding all 4 096 envs and the concatenated rollout;
+      - every AdamW step's parameters within 1e-4 relative to the change so
+        far (65 536 fixed positions), and the end state within 1e-4."""
+    if not torch.cuda.is_available():
+        pytest.fail("gpu tests need a HIP device")
+    from oracle import oracle as O
+    from tests.torch_ref import unpack_bits
+    from vmp.ppo import PPOTrainer
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    tmp = str(tmp_path)
+    procs = [ctx.Process(target=_share_worker, args=(r, SHARE_WORLD, port, tmp, q))
+             for r in range(SHARE_WORLD)]
+    for p in procs:
+        p.start()
+    meta = {}
+    for _ in procs:
+        r, seed, n_mb, n_kl = q.get(timeout=400)
+        meta[r] = (seed, n_mb, n_kl)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert meta[0][0] != meta[1][0]  # rank-folded sampling streams
+    roll = [dict(np.load(os.path.join(tmp, f"roll{r}.npz"))) for r in range(SHARE_WORLD)]
+    res = [dict(np.load(os.path.join(tmp, f"res{r}.npz"))) for r in range(SHARE_WORLD)]
+    assert np.array_equal(res[0]["p0_full"], res[1]["p0_full"])
+    assert np.array_equal(res[0]["p1_full"], res[1]["p1_full"])  # ranks identical after 16 steps
+    assert np.array_equal(res[0]["g"], res[1]["g"])
+    V, A, T = 300, 102, roll[0]["rew"].shape[0]
+    # every sampled action is valid
+    for r in range(SHARE_WORLD):
+        bits = torch.from_numpy(roll[r]["bits"]).to(DEV)
+        act = torch.from_numpy(roll[r]["act"]).to(DEV).long()
+        for t in range(T):
+            full = unpack_bits(bits[t], A)
+            assert not full.gather(-1, act[t][..., None]).any(), (r, t)
+    # 2 envs of each rank through the C oracle (global index r * 2048 + i, seed 4 * gi)
+    for r in range(SHARE_WORLD):
+        for i in (0, N_SHARE - 1 - 17 * r):
+            gi = r * N_SHARE + i
+            e = O.OracleEnv(dict(CFG100, seed=4 * gi))
+            e.eval(False)
+            e.reset(4 * gi)
+            full = unpack_bits(torch.from_numpy(roll[r]["bits"][:, i]), A).numpy()
+            for t in range(T):
+                assert np.array_equal(e.obs(), roll[r]["obs"][t, i]), (r, i, t)
+                assert np.array_equal(e.mask(), full[t]), (r, i, t)
+                o, rew, _, _ = e.step(roll[r]["act"][t, i].astype(np.int64))
+                assert np.float32(rew) == roll[r]["rew"][t, i], (r, i, t)
+            assert np.array_equal(o, roll[r]["last_obs"][i]), (r, i)
+            assert np.array_equal(e.counters()[0], roll[r]["counters"][i]), (r, i)
+    # one process holding all 4 096 envs, the concatenated rollout
+    n_glob = SHARE_WORLD * N_SHARE
+    env, ag = _agent(n_glob)
+    assert np.array_equal(_flat_params(ag.model).cpu().numpy(), res[0]["p0_full"])
+    tr = PPOTrainer(ag, distributed=False)
+    for k in BUFS:
+        cat = np.concatenate([roll[r][k] for r in range(SHARE_WORLD)],
+                             axis=0 if k == "last_obs" else 1)
+        getattr(tr, k).copy_(torch.from_numpy(cat).to(DEV))
+        del cat
+    del roll
+    idx = torch.from_numpy(res[0]["idx"]).to(DEV)
+    trace = {}
+    _install_dp_trace(ag, idx, trace)
+    st = tr.update()
+    assert st["minibatches"] == meta[0][1] and st["kl_breaks"] == meta[0][2]
+    g_rel = np.linalg.norm(res[0]["g"] - trace["g"]) / np.linalg.norm(trace["g"])
+    p0 = res[0]["p0"]
+    ours, ref = res[0]["steps"], np.stack(trace["p"])
+    assert ours.shape == ref.shape
+    step_rel = [float(np.linalg.norm(ours[s] - ref[s]) / np.linalg.norm(ref[s] - p0))
+                for s in range(len(ref))]
+    p1 = _flat_params(ag.model).double().cpu().numpy()
+    d = res[0]["p1_full"].astype(np.float64) - p1
+    c = p1 - res[0]["p0_full"]
+    end_rel = float(np.linalg.norm(d) / np.linalg.norm(c))
+    print(f"config 4 at 2 x 2048 envs: first-step gradient rel L2 {g_rel:.2e}; per-step "
+          f"parameter rel {max(step_rel):.2e} (max over {len(step_rel)} steps); end state rel "
+          f"{end_rel:.2e}, max |diff| {np.abs(d).max():.2e}, max |change| {np.abs(c).max():.2e}")
+    env.close()
+    assert np.abs(c).max() > 1e-4
+    assert g_rel <= 3e-5, g_rel
+    assert max(step_rel) <= 1e-4, step_rel
+    assert end_rel <= 1e-4, end_rel

@@ -1,0 +1,99 @@
+"""The bf16 training head at the config/100.yml update shape (one minibatch of
+8192 envs x 25 steps = 204 800 samples, K 512, V 300, A 102):
+  fused   vmp_actor_head_bf16_fwd, then per backward chunk vmp_actor_head_bf16_bwd
+          + dh / [dW | db] GEMMs (BF16FusedActorHead)
+  logits  hipBLASLt bf16 GEMM -> f32 logits + tiled head, head backward -> bf16
+          dlogits + GEMMs + bias column sum (BF16ActorHead)
+HIP events per stage; TFLOP/s of the head GEMM work (2 B K N per product).
+Usage: python tools/bench_actor_head_bf16.py [B]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "vm-placement-migration-gym_amd")]
+import torch  # noqa: E402
+
+from vmp import head as H  # noqa: E402
+from vmp.ppo import BF16ActorHead, BF16FusedActorHead  # noqa: E402
+
+
+def timeit(fn, n=5, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def main():
+    dev = "cuda:0"
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 204800
+    K, V, A = 512, 300, 102
+    N = V * A
+    g = torch.Generator(device=dev).manual_seed(0)
+    h = torch.tanh(torch.randn((B, K), device=dev, generator=g))
+    w = torch.randn((N, K), device=dev, generator=g) * 0.05
+    b = torch.randn((N,), device=dev, generator=g) * 0.1
+    bits = torch.zeros((B, V, 4), dtype=torch.int32, device=dev)
+    for i in range(0, B, 16384):  # random masks, chunked (the bool mask is large)
+        m = torch.rand((min(B, i + 16384) - i, V, A), device=dev, generator=g) < 0.5
+        m[..., A - 2] = False
+        bits[i:i + m.shape[0]] = H.pack_mask(m, V, A)
+    act = torch.randint(0, A - 2, (B, V), device=dev, dtype=torch.int32)
+    hb = h.bfloat16()
+    wb = w.bfloat16()
+    glp = torch.randn(B, device=dev, generator=g)
+    gen = torch.randn(B, device=dev, generator=g) * 0.01
+    flop = 2.0 * B * K * N
+    out = {"B": B, "K": K, "V": V, "A": A}
+
+    t = timeit(lambda: H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act))
+    out["fused_fwd_ms"] = t
+    out["fused_fwd_tflops"] = flop / t / 1e9
+    rows = (1 << 32) // (2 * N) // 256 * 256
+    dl = torch.empty((rows, N), dtype=torch.bfloat16, device=dev)
+    r = min(rows, B)
+    t = timeit(lambda: H.actor_head_bf16_bwd(hb[:r], wb, b, V, A, bits[:r], act[:r], glp[:r],
+                                             gen[:r], dl))
+    out["fused_bwd_kernel_ms_per_chunk"] = t
+    out["fused_bwd_kernel_tflops"] = 2.0 * r * K * N / t / 1e9
+    out["chunk_rows"] = r
+
+    def fused_full():
+        x = h.detach().requires_grad_(True)
+        ww = w.detach().requires_grad_(True)
+        bb = b.detach().requires_grad_(True)
+        lp, ent = BF16FusedActorHead.apply(x, ww, bb, bits, act, V, A, rows)
+        torch.autograd.backward([lp, ent], [glp, gen])
+
+    def logits_full():
+        x = h.detach().requires_grad_(True)
+        ww = w.detach().requires_grad_(True)
+        bb = b.detach().requires_grad_(True)
+        lp, ent = BF16ActorHead.apply(x, ww, bb, bits, act, V, A)
+        torch.autograd.backward([lp, ent], [glp, gen])
+
+    torch.cuda.reset_peak_memory_stats()
+    t = timeit(fused_full, n=3, warm=1)
+    out["fused_fwd_bwd_ms"] = t
+    out["fused_fwd_bwd_tflops_useful"] = 3 * flop / t / 1e9
+    out["fused_peak_gb"] = torch.cuda.max_memory_allocated() / 1e9
+    del dl
+    torch.cuda.empty_cache()
+    if os.environ.get("SKIP_LOGITS") != "1":
+        torch.cuda.reset_peak_memory_stats()
+        t = timeit(logits_full, n=3, warm=1)
+        out["logits_fwd_bwd_ms"] = t
+        out["logits_fwd_bwd_tflops_useful"] = 3 * flop / t / 1e9
+        out["logits_peak_gb"] = torch.cuda.max_memory_allocated() / 1e9
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

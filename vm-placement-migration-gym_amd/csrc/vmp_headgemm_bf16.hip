@@ -1,0 +1,423 @@
+// vmp_headgemm_bf16.hip — the training side of the fused actor head
+// (src/agents/ppo.py:115-126 get_action(obs, action, mask) and
+// the PPOAgent.update backward through it, ppo.py:258-287), on the bf16
+// matrix cores.
+//
+// Forward (GIVEN actions): logits = h W^T + b are formed tile by tile with
+// v_mfma_f32_16x16x32_bf16 (bf16 h and W, f32 accumulate) and consumed in
+// registers: masked max / sum / lse, entropy lse - (sum p x)/S and the given
+// action's logprob per (sample, VM row) -> row buffers -> k_rowsum. The
+// [B, V*A] logits never reach HBM.
+// Backward: the same tiles are recomputed, and dlogits
+//   d_j = -q_j (g_lp + g_ent (x_j - lse + H)) + g_lp [j = a],  0 at masked j
+// is formed in registers and rounded to bf16 for the dW / dh GEMMs, written
+// for the caller's row chunk only (the host runs the backward chunk by chunk,
+// so at most one chunk of dlogits exists; the bias gradient comes out of the
+// dW GEMM as the product with a column of ones appended to h).
+//
+// Tile: a workgroup of 8 waves owns BM = 256 samples x NT 16-column tiles.
+// The columns are S whole action segments, each padded to SA = 16 TS columns
+// (TS tiles), so a tile column's segment is known at compile time: tile
+// column n = 16 TS s + j holds logit j of VM row v0 + s. Wave w owns samples
+// 32w..32w+31; the accumulators are computed transposed (W as the A operand):
+// lane (q = l >> 4, c = l & 15) holds columns 16 nt + 4q + 0..3 of sample
+// 16 mc + c, so a segment's row reductions are in-lane sums plus two xor
+// shuffles over q. Operands are staged through LDS with global_load_lds
+// (16 B per lane, two stages of BK = 64; 128-B rows, 16-B chunk index XOR
+// (row >> 1) & 7 on the source address and on the read: conflict-free
+// ds_read_b128 fragments). The bias is the accumulators' initial value.
+//
+// Each workgroup keeps one column tile and loops over the M blocks of its M
+// group; workgroups of one XCD run the same M block at about the same time,
+// so the h tile is an L2 hit for all but the first.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "../../include/vmp.h"
+
+#define LDSP __attribute__((address_space(3)))
+#define GLBP __attribute__((address_space(1)))
+
+namespace vmp {
+
+__global__ void k_rowsum(int B, int V, const float *row_lp, const float *row_ent, float *lp,
+                         float *ent);
+int policy_fail(int code, const char *msg);
+
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 256;       // samples per M block (NW waves x MC 16-sample columns)
+constexpr int kBK = 64;        // K per LDS stage
+constexpr int kRow = 2 * kBK;  // bytes per staged row
+constexpr int kMaxNT = 14;     // 16-column accumulator tiles per workgroup
+constexpr float kMasked = -1e7f;   // ppo.py:119
+constexpr float kPad = -1e30f;     // tile columns past A: p = 0, never the max
+constexpr float kLog2e = 1.44269504088896341f;
+
+struct H16Args {
+  int B, K, V, A, W32, n_tiles, m_blocks, m_groups, ld;
+  const uint16_t *h, *w;
+  const float *bias;
+  const uint32_t *bits;
+  const int32_t *action;
+  const float *g_lp, *g_ent;
+  float *row_lp, *row_ent;  // forward: per (sample, VM row)
+  uint16_t *dl;             // backward: bf16 dlogits [B][ld]
+};
+
+__device__ __forceinline__ int lds_chunk(int row, int cl) { return cl ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ bf16x8 frag(const char LDSP *base, int row, int cl) {
+  return *reinterpret_cast<const bf16x8 LDSP *>(base + row * kRow + (lds_chunk(row, cl) << 4));
+}
+
+// global -> LDS staging of one K stage: W rows (tile columns, segment-padded)
+// then h rows, 8 rows of 128 B per wave instruction; lane L writes LDS
+// position L % 8 of row L / 8 with the logical chunk that position holds.
+template <int TS, int NT, int NW>
+__device__ __forceinline__ void stage_issue(const H16Args &a, char LDSP *buf, int v0, int m0,
+                                            int k0, int wid, int lane) {
+  constexpr int SA = 16 * TS, BNp = 16 * NT, PW = BNp / 8, PIECES = (BNp + kBM) / 8;
+  const int rl = lane >> 3, p = lane & 7;
+#pragma unroll
+  for (int i0 = 0; i0 < PIECES; i0 += NW) {
+    const int i = i0 + wid;
+    if (i < PIECES) {  // wave-uniform
+      const uint16_t *src;
+      int r;
+      if (i < PW) {
+        r = 8 * i + rl;
+        const int s = r / SA, j = r - s * SA;
+        const int v = v0 + s;
+        const int wr = (v < a.V && j < a.A) ? v * a.A + j : v0 * a.A;  // pad rows: any row
+        src = a.w + (int64_t)wr * a.K;
+      } else {
+        r = 8 * (i - PW) + rl;
+        src = a.h + (int64_t)min(m0 + r, a.B - 1) * a.K;
+      }
+      src += k0 + 8 * lds_chunk(r, p);
+      char LDSP *dst = buf + (i < PW ? 0 : BNp * kRow) + (r - rl) * kRow;
+      __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)dst, 16, 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ float xsum(float v) {
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+__device__ __forceinline__ float xmax(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16));
+  return fmaxf(v, __shfl_xor(v, 32));
+}
+
+// the row's mask words (bit j of word j >> 5 = action j invalid), bits past A cleared
+__device__ __forceinline__ void load_mask(const H16Args &a, int64_t row, uint32_t (&mw)[4]) {
+  mw[0] = mw[1] = mw[2] = mw[3] = 0u;
+  if (!a.bits) return;
+  const uint32_t *src = a.bits + row * a.W32;
+  if (a.W32 == 4) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(src);
+    mw[0] = v.x, mw[1] = v.y, mw[2] = v.z, mw[3] = v.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (i < a.W32) mw[i] = src[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int tail = a.A - 32 * i;
+    mw[i] &= tail >= 32 ? ~0u : (tail > 0 ? (1u << tail) - 1u : 0u);
+  }
+}
+
+// NW waves per workgroup, each owning MC = 16 / NW columns of 16 samples
+// (built: 8 waves x 2 columns, two waves per SIMD)
+template <int TS, bool BWD, int NW>
+__global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
+  constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
+  constexpr int MC = 16 / NW, kThreads = 64 * NW;
+  constexpr int kStageW = BNp * kRow, kStage = kStageW + kBM * kRow;
+  extern __shared__ __align__(16) char lds_raw[];
+  char LDSP *lds = (char LDSP *)lds_raw;
+  float LDSP *biasL = reinterpret_cast<float LDSP *>(lds + 2 * kStage);
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  const int n_tile = blockIdx.x % a.n_tiles, g = blockIdx.x / a.n_tiles;
+  const int v0 = n_tile * S;
+
+  // the tile's bias in tile-column order (0 past A / past V)
+  for (int n = t; n < BNp; n += kThreads) {
+    const int s = n / SA, j = n - s * SA, v = v0 + s;
+    biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
+  }
+  __syncthreads();
+
+  const int nk = a.K / kBK;
+
+#pragma unroll 1
+  for (int mb = g; mb < a.m_blocks; mb += a.m_groups) {
+    const int m0 = mb * kBM;
+    f32x4 acc[NT][MC];
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
+#pragma unroll
+      for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
+    }
+    // ---- GEMM: two LDS stages, the next stage's DMA under this stage's MFMAs ----
+    stage_issue<TS, NT, NW>(a, lds, v0, m0, 0, wid, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll 1
+    for (int s = 0; s < nk; s++) {
+      const char LDSP *cur = lds + (s & 1) * kStage;
+      if (s + 1 < nk)
+        stage_issue<TS, NT, NW>(a, lds + ((s + 1) & 1) * kStage, v0, m0, (s + 1) * kBK, wid, lane);
+      const char LDSP *Hs = cur + kStageW;
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++) {
+        const int cl = 4 * kk + q;
+        bf16x8 hf[MC];
+#pragma unroll
+        for (int mc = 0; mc < MC; mc++) hf[mc] = frag(Hs, 16 * (MC * wid + mc) + c, cl);
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) {
+          const bf16x8 wf = frag(cur, 16 * nt + c, cl);
+#pragma unroll
+          for (int mc = 0; mc < MC; mc++)
+            acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hf[mc], acc[nt][mc], 0, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+
+    // ---- epilogue: per sample column mc, per segment s, in registers ----
+#pragma unroll
+    for (int mc = 0; mc < MC; mc++) {
+      const int m = m0 + 16 * (MC * wid + mc) + c;
+      const bool live = m < a.B;
+      const int mm = live ? m : a.B - 1;
+      float glp = 0.f, gen = 0.f;
+      if (BWD) {
+        glp = a.g_lp ? a.g_lp[mm] : 0.f;
+        gen = a.g_ent ? a.g_ent[mm] : 0.f;
+      }
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        const int v = v0 + s;
+        if (v >= a.V) break;  // workgroup-uniform: the last tile's missing segments
+        const int64_t row = (int64_t)mm * a.V + v;
+        uint32_t mw[4];
+        load_mask(a, row, mw);
+        const int act = a.action[row];
+        const int tgt = (act >= 0 && act < a.A) ? act : -1;
+        // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
+        float xm[TS][4];
+        uint32_t nib[TS];
+        float mx = kPad;
+#pragma unroll
+        for (int u = 0; u < TS; u++) {
+          nib[u] = mw[u >> 1] >> (16 * (u & 1) + 4 * q);
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int j = 16 * u + 4 * q + r;
+            const float x = ((nib[u] >> r) & 1u) ? kMasked : acc[s * TS + u][mc][r];
+            xm[u][r] = j < a.A ? x : kPad;
+            mx = fmaxf(mx, xm[u][r]);
+          }
+        }
+        mx = xmax(mx);
+        // pass 2: p = exp(x - m) (x - m first: exact at x = m, so an all-masked
+        // row gets p = 1 everywhere, as the unfused head), S, T = sum p x
+        float p[TS][4];
+        float Ss = 0.f, Ts = 0.f, xa = 0.f;
+#pragma unroll
+        for (int u = 0; u < TS; u++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            p[u][r] = __builtin_amdgcn_exp2f((xm[u][r] - mx) * kLog2e);
+            Ss += p[u][r];
+            Ts = __builtin_fmaf(p[u][r], xm[u][r], Ts);
+            if (!BWD) xa = (16 * u + 4 * q + r == tgt) ? xm[u][r] : xa;
+          }
+        Ss = xsum(Ss);
+        Ts = xsum(Ts);
+        const float lse = mx + logf(Ss);
+        const float inv = 1.0f / Ss;
+        const float H = lse - Ts * inv;  // Categorical.entropy, the tiled head's order
+        if (!BWD) {
+          xa = xsum(xa);  // one lane-element holds it, the others 0
+          if (live && q == 0) {
+            a.row_lp[row] = tgt >= 0 ? xa - lse : NAN;
+            a.row_ent[row] = H;
+          }
+        } else {
+          const float c1 = glp + gen * (H - lse);
+#pragma unroll
+          for (int u = 0; u < TS; u++) {
+            float d[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              const int j = 16 * u + 4 * q + r;
+              float dd = -(p[u][r] * inv) * __builtin_fmaf(gen, xm[u][r], c1);
+              dd += (j == tgt) ? glp : 0.f;
+              d[r] = (j < a.A && !((nib[u] >> r) & 1u)) ? dd : 0.f;
+            }
+            // bf16 dlogits (round to nearest even), columns v A + j of row m
+            const int j0 = 16 * u + 4 * q;
+            if (live && j0 < a.A) {
+              uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
+              const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
+              const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
+              const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
+              if (((a.A | a.ld) & 1) == 0 && j0 + 3 < a.A) {  // two 4-B stores
+                *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
+                *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
+              } else {
+                dst[0] = u0;
+                if (j0 + 1 < a.A) dst[1] = u1;
+                if (j0 + 2 < a.A) dst[2] = u2;
+                if (j0 + 3 < a.A) dst[3] = u3;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int TS>
+constexpr size_t lds_bytes() {
+  return 2 * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow + 16 * (kMaxNT / TS * TS) * sizeof(float);
+}
+
+int pick_ts(int A) {  // the smallest built segment width (16 TS columns) that holds A
+  if (A <= 16) return 1;
+  if (A <= 32) return 2;
+  if (A <= 64) return 4;
+  if (A <= 112) return 7;
+  return 8;
+}
+
+// M groups: the grid is n_tiles x m_groups workgroups at one per CU; pick the
+// group count whose last dispatch round is fullest (ties: fewer workgroups)
+int pick_groups(int n_tiles, int m_blocks) {
+  int best = 1;
+  double best_eff = -1.0;
+  for (int g = 1; g <= m_blocks && g <= 64; g++) {
+    const int64_t wg = (int64_t)n_tiles * g;
+    const double rounds = (double)((wg + 255) / 256);
+    const double eff = (double)wg / (rounds * 256.0);
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = g;
+    }
+    if (eff > 0.97) break;
+  }
+  return best;
+}
+
+template <bool BWD, int NW>
+hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
+  const dim3 grid((unsigned)((int64_t)a.n_tiles * a.m_groups)), block(64 * NW);
+  switch (TS) {
+    case 1: hipLaunchKernelGGL((k_hg16<1, BWD, NW>), grid, block, lds_bytes<1>(), st, a); break;
+    case 2: hipLaunchKernelGGL((k_hg16<2, BWD, NW>), grid, block, lds_bytes<2>(), st, a); break;
+    case 4: hipLaunchKernelGGL((k_hg16<4, BWD, NW>), grid, block, lds_bytes<4>(), st, a); break;
+    case 7: hipLaunchKernelGGL((k_hg16<7, BWD, NW>), grid, block, lds_bytes<7>(), st, a); break;
+    default: hipLaunchKernelGGL((k_hg16<8, BWD, NW>), grid, block, lds_bytes<8>(), st, a); break;
+  }
+  return hipGetLastError();
+}
+
+template <bool BWD>
+hipError_t launch_hg16(H16Args &a, hipStream_t st) {
+  const int TS = pick_ts(a.A);
+  const int S = kMaxNT / TS;
+  a.n_tiles = (a.V + S - 1) / S;
+  a.m_blocks = (a.B + kBM - 1) / kBM;
+  a.m_groups = pick_groups(a.n_tiles, a.m_blocks);
+  return launch_ts<BWD, 8>(a, TS, st);
+}
+
+int check_common(int32_t B, int32_t K, int32_t V, int32_t A, const void *h, const void *w,
+                 const float *bias, const int32_t *action, const char *who) {
+  if (B < 0 || K < 1 || V < 1 || A < 1 || !h || !w || !bias || !action)
+    return policy_fail(VMP_EINVAL, who);
+  if (K % kBK != 0 || A > VMP_ACTOR_HEAD_MAX_A)
+    return policy_fail(VMP_EINVAL, "bf16 actor head: needs K % 64 == 0 and A <= 128");
+  if ((((uintptr_t)h) | ((uintptr_t)w)) & 15)
+    return policy_fail(VMP_EINVAL, "bf16 actor head: h and weight must be 16-byte aligned");
+  return VMP_OK;
+}
+
+}  // namespace
+}  // namespace vmp
+
+using namespace vmp;
+
+extern "C" int vmp_actor_head_bf16_fwd(int32_t B, int32_t K, int32_t V, int32_t A,
+                                       const uint16_t *h, const uint16_t *weight,
+                                       const float *bias, const uint32_t *mask_bits,
+                                       const int32_t *action, float *logprob, float *entropy,
+                                       float *workspace, void *stream) {
+  int rc = check_common(B, K, V, A, h, weight, bias, action,
+                        "vmp_actor_head_bf16_fwd: bad shape or null pointer");
+  if (rc) return rc;
+  if (!logprob || !entropy) return policy_fail(VMP_EINVAL, "vmp_actor_head_bf16_fwd: null output");
+  if (B == 0) return VMP_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t rows = (int64_t)B * V;
+  float *scratch = nullptr, *ws = workspace;
+  if (!ws) {
+    hipError_t e = hipMallocAsync((void **)&scratch, 2 * rows * sizeof(float), st);
+    if (e != hipSuccess) return policy_fail(VMP_EOOM, hipGetErrorString(e));
+    ws = scratch;
+  }
+  H16Args a{};
+  a.B = B, a.K = K, a.V = V, a.A = A, a.W32 = (A + 31) / 32, a.ld = V * A;
+  a.h = h, a.w = weight, a.bias = bias, a.bits = mask_bits, a.action = action;
+  a.row_lp = ws, a.row_ent = ws + rows;
+  hipError_t e = launch_hg16<false>(a, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_rowsum, dim3((B + 3) / 4), dim3(256), 0, st, B, V, a.row_lp, a.row_ent,
+                       logprob, entropy);
+    e = hipGetLastError();
+  }
+  if (scratch) {
+    hipError_t f = hipFreeAsync(scratch, st);
+    if (e == hipSuccess) e = f;
+  }
+  if (e != hipSuccess) return policy_fail(VMP_EDEVICE, hipGetErrorString(e));
+  return VMP_OK;
+}
+
+extern "C" int vmp_actor_head_bf16_bwd(int32_t B, int32_t K, int32_t V, int32_t A,
+                                       const uint16_t *h, const uint16_t *weight,
+                                       const float *bias, const uint32_t *mask_bits,
+                                       const int32_t *action, const float *g_logprob,
+                                       const float *g_entropy, uint16_t *dlogits, int32_t ld,
+                                       void *stream) {
+  int rc = check_common(B, K, V, A, h, weight, bias, action,
+                        "vmp_actor_head_bf16_bwd: bad shape or null pointer");
+  if (rc) return rc;
+  if (!dlogits || ld < V * A)
+    return policy_fail(VMP_EINVAL, "vmp_actor_head_bf16_bwd: null dlogits or ld < V*A");
+  if (B == 0) return VMP_OK;
+  H16Args a{};
+  a.B = B, a.K = K, a.V = V, a.A = A, a.W32 = (A + 31) / 32, a.ld = ld;
+  a.h = h, a.w = weight, a.bias = bias, a.bits = mask_bits, a.action = action;
+  a.g_lp = g_logprob, a.g_ent = g_entropy, a.dl = dlogits;
+  hipError_t e = launch_hg16<true>(a, (hipStream_t)stream);
+  if (e != hipSuccess) return policy_fail(VMP_EDEVICE, hipGetErrorString(e));
+  return VMP_OK;
+}

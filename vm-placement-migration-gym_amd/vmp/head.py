@@ -236,6 +236,45 @@ def actor_head(h, weight, bias, V, A, bits=None, action=None, rng: HeadRng = Non
     return act, lp, ent
 
 
+def actor_head_bf16_supported(K, A):
+    """vmp_actor_head_bf16_fwd/_bwd's shape contract (include/vmp.h)."""
+    return K % 64 == 0 and A <= ACTOR_HEAD_MAX_A
+
+
+def actor_head_bf16_fwd(hb, wb, bias, V, A, bits, action):
+    """The bf16 training forward (vmp_actor_head_bf16_fwd): hb bf16 [B, K], wb bf16
+    [V*A, K], bias f32 [V*A], GIVEN actions -> (logprob [B], entropy [B]); the
+    logits are consumed in registers, never written."""
+    _need_device(hb, "actor_head_bf16_fwd")
+    B, K = hb.shape
+    if bits is not None and tuple(bits.shape) != (B, V, (A + 31) // 32):
+        raise ValueError(f"mask bits {tuple(bits.shape)} != {(B, V, (A + 31) // 32)}")
+    act = action.to(device=hb.device, dtype=torch.int32).reshape(B, V).contiguous()
+    lp = torch.empty((B,), dtype=torch.float32, device=hb.device)
+    ent = torch.empty((B,), dtype=torch.float32, device=hb.device)
+    ws = torch.empty((2 * B * V,), dtype=torch.float32, device=hb.device)
+    check(lib().vmp_actor_head_bf16_fwd(B, K, V, A, ptr(hb), ptr(wb), ptr(bias.contiguous()),
+                                        ptr(bits), ptr(act), ptr(lp), ptr(ent), ptr(ws),
+                                        _stream(hb)))
+    return act, lp, ent
+
+
+def actor_head_bf16_bwd(hb, wb, bias, V, A, bits, action, g_lp, g_ent, out):
+    """The bf16 training backward (vmp_actor_head_bf16_bwd) over the rows of hb
+    (a chunk): recomputes the logits tiles and writes bf16 dlogits into `out`
+    ([rows, >= V*A], row stride out.stride(0))."""
+    _need_device(hb, "actor_head_bf16_bwd")
+    B, K = hb.shape
+    if out.dtype != torch.bfloat16 or out.shape[0] < B or out.stride(1) != 1:
+        raise ValueError("dlogits out must be bf16 [rows, V*A] with unit column stride")
+    glp = None if g_lp is None else g_lp.float().contiguous()
+    gen = None if g_ent is None else g_ent.float().contiguous()
+    check(lib().vmp_actor_head_bf16_bwd(B, K, V, A, ptr(hb), ptr(wb), ptr(bias.contiguous()),
+                                        ptr(bits), ptr(action), ptr(glp), ptr(gen), ptr(out),
+                                        int(out.stride(0)), _stream(hb)))
+    return out
+
+
 def det_action(logits, V, A):
     """get_det_action (ppo.py:128-131): unmasked argmax per VM row -> int32 [B, V]."""
     _need_device(logits, "det_action")

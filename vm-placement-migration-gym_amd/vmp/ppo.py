@@ -67,6 +67,7 @@ class PPOConfig:
     value_loss_broadcast: bool = True  # ppo.py:266-270 [mb,1]-[mb] broadcast
     precision: str = "f32"             # "bf16": bf16 GEMM inputs, f32 accumulate/output
     chunk_bytes: int = 0               # logits budget per update chunk (0: from free HBM, fixed at the first update)
+    dlogits_chunk_bytes: int = 1 << 32  # bf16 fused head: dlogits rows per backward chunk
     seed_stride: int = 4               # env/episode reset seed spacing
 
 
@@ -178,6 +179,59 @@ class BF16ActorHead(torch.autograd.Function):
         return gx, gw, gb, None, None, None, None
 
 
+class BF16FusedActorHead(torch.autograd.Function):
+    """The bf16 leg's last actor Linear + masked head (GIVEN actions) on the HIP
+    bf16 matrix-core kernels (vmp_actor_head_bf16_fwd/_bwd):
+    the forward consumes each logits tile in registers; the backward recomputes
+    the tiles chunk by chunk (`chunk_rows` samples at a time) and writes only
+    that chunk's bf16 dlogits, which two GEMMs turn into dh and [dW | db] (the
+    bias gradient is the product with a column of ones appended to h). No
+    [B, V*A] tensor is allocated in either direction."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, bits, action, V, A, chunk_rows):
+        xb, wb = x.to(torch.bfloat16).contiguous(), _bf16_weight(w)
+        act, lp, ent = H.actor_head_bf16_fwd(xb, wb, b, V, A, bits, action)
+        ctx.save_for_backward(xb, wb, b, bits, act)
+        ctx.V, ctx.A, ctx.chunk_rows = V, A, int(chunk_rows)
+        return lp, ent
+
+    @staticmethod
+    def backward(ctx, g_lp, g_ent):
+        xb, wb, b, bits, act = ctx.saved_tensors
+        V, A = ctx.V, ctx.A
+        B, K = xb.shape
+        N = V * A
+        R = max(1, min(B, ctx.chunk_rows))
+        dev = xb.device
+        glp = torch.zeros(B, device=dev) if g_lp is None else g_lp.float().contiguous()
+        gen = torch.zeros(B, device=dev) if g_ent is None else g_ent.float().contiguous()
+        need_x, need_w, need_b = ctx.needs_input_grad[:3]
+        dl = torch.empty((R, N), dtype=torch.bfloat16, device=dev)
+        gx = torch.empty((B, K), dtype=torch.float32, device=dev) if need_x else None
+        # h | 1 | 0...: the dW GEMM's extra output column K is the bias gradient
+        KA = K + 8
+        haug = torch.zeros((R, KA), dtype=torch.bfloat16, device=dev)
+        haug[:, K] = 1.0
+        gwa = None
+        for r0 in range(0, B, R):
+            r1 = min(B, r0 + R)
+            n = r1 - r0
+            d = dl[:n]
+            H.actor_head_bf16_bwd(xb[r0:r1], wb, b, V, A, None if bits is None else bits[r0:r1],
+                                  act[r0:r1], glp[r0:r1], gen[r0:r1], d)
+            if need_x:
+                gx[r0:r1] = torch.mm(d, wb, out_dtype=torch.float32)
+            if need_w or need_b:
+                ha = haug[:n]
+                ha[:, :K] = xb[r0:r1]
+                part = torch.mm(d.t(), ha, out_dtype=torch.float32)
+                gwa = part if gwa is None else gwa.add_(part)
+        gw = gwa[:, :K].contiguous() if need_w else None
+        gb = gwa[:, K].contiguous() if need_b else None
+        return gx, gw, gb, None, None, None, None, None
+
+
 def _run_mlp(seq, x, precision):
     if precision != "bf16":
         return seq(x)
@@ -265,14 +319,34 @@ class Network(nn.Module):
             return act
         return H.det_action(self.actor_logits(obs), self.V, self.A)
 
-    def logprob_entropy(self, obs, bits, action):
+    def bf16_fused(self):
+        """The bf16 update runs the fused matrix-core head (BF16FusedActorHead)
+        where its kernels apply; VMP_BF16_FUSED=0 selects the logits path
+        (BF16ActorHead) for A/B measurement."""
+        last = self.actor[-1]
+        return (self.precision == "bf16" and self._head is H.policy_head
+                and os.environ.get("VMP_BF16_FUSED", "1") != "0"
+                and H.actor_head_bf16_supported(last.in_features, self.A))
+
+    def logits_bytes_per_sample(self):
+        """HBM the update's head needs per sample beyond activations: the f32
+        logits (and their gradient) of the logits paths; ~0 on the fused one."""
+        return 0 if self.bf16_fused() else 4 * self.V * self.A
+
+    def logprob_entropy(self, obs, bits, action, dlogits_chunk_bytes=1 << 32):
         """get_action(obs, action, mask)'s logprob and entropy (ppo.py:115-126) for
         the update, differentiable. The bf16 leg with the HIP head runs the last
-        Linear and the head as one node (BF16ActorHead)."""
+        Linear and the head as one node: fused on the bf16 matrix cores
+        (BF16FusedActorHead, the backward's dlogits chunked to
+        `dlogits_chunk_bytes`), else over f32 logits (BF16ActorHead)."""
         if (self.precision == "bf16" and self._head is H.policy_head and obs.is_cuda
                 and self.A <= H.HEAD_TILE_MAX_A):
             last = self.actor[-1]
             h = _run_mlp(self.actor[:-1], obs, "bf16")
+            if self.bf16_fused():
+                rows = max(256, int(dlogits_chunk_bytes) // (2 * self.V * self.A) // 256 * 256)
+                return BF16FusedActorHead.apply(h, last.weight, last.bias, bits, action, self.V,
+                                                self.A, rows)
             return BF16ActorHead.apply(h, last.weight, last.bias, bits, action, self.V, self.A)
         _, lp, ent = self._head(self.actor_logits(obs), self.V, self.A, bits=bits, action=action,
                                 rng=self.rng)
@@ -610,7 +684,6 @@ class PPOTrainer:
             adv, ret = self.gae(rew, done, values, next_values, cfg.gamma, cfg.lamda)
         mbs = int(cfg.minibatch_size)
         n_mb = math.ceil(T / mbs)
-        VA = self.V * self.A
         eps = cfg.eps_clip
         params = [p for p in m.parameters()]
         stats = dict(minibatches=0, kl_breaks=0, clipfracs=[])
@@ -627,7 +700,8 @@ class PPOTrainer:
                     ss = self._allreduce(((a_mb - mean) ** 2).sum().reshape(1).double())
                     std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
                     adv_n = (a_mb - mean) / (std + 1e-10)
-                ce = max(1, min(N, self._chunk_budget(rew.device) // max(1, mt * VA * 4)))
+                per_env = mt * m.logits_bytes_per_sample()
+                ce = N if per_env == 0 else max(1, min(N, self._chunk_budget(rew.device) // per_env))
                 self._zero_grads(params)
                 kl_sum = torch.zeros(1, dtype=torch.float64, device=rew.device)
                 clip_n = torch.zeros(1, dtype=torch.float64, device=rew.device)
@@ -637,7 +711,7 @@ class PPOTrainer:
                     o = obs[t0:t1, n0:n1].reshape(mt * nc, -1)
                     b = None if bits is None else bits[t0:t1, n0:n1].reshape(mt * nc, self.V, -1)
                     a = act[t0:t1, n0:n1].reshape(mt * nc, self.V)
-                    newlp, ent = m.logprob_entropy(o, b, a)
+                    newlp, ent = m.logprob_entropy(o, b, a, cfg.dlogits_chunk_bytes)
                     newlp = newlp.reshape(mt, nc)
                     logratio = newlp - old_lp[t0:t1, n0:n1]
                     ratio = torch.exp(logratio)
