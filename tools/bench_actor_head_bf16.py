@@ -53,6 +53,29 @@ def main():
     flop = 2.0 * B * K * N
     out = {"B": B, "K": K, "V": V, "A": A}
 
+    if os.environ.get("FWD_ONLY") == "1":  # variant A/B: the fused kernels alone
+        t = timeit(lambda: H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act), n=10)
+        r = min(B, 70144)
+        dl = torch.empty((r, N), dtype=torch.bfloat16, device=dev)
+        tb = timeit(lambda: H.actor_head_bf16_bwd(hb[:r], wb, b, V, A, bits[:r], act[:r], glp[:r],
+                                                  gen[:r], dl), n=10)
+        print(json.dumps({"lib": os.environ.get("VMP_LIB_PATH", "default").split("/")[-1],
+                          "fused_fwd_ms": t, "fused_fwd_tflops": flop / t / 1e9,
+                          "bwd_ms_per_204800": tb * B / r,
+                          "bwd_tflops": 2.0 * r * K * N / tb / 1e9}), flush=True)
+        return
+    # hipBLASLt on the same GEMM: f32 logits out (what the logits path writes), bf16 out
+    lg = torch.empty((B, N), dtype=torch.float32, device=dev)
+    t = timeit(lambda: torch.mm(hb, wb.t(), out_dtype=torch.float32, out=lg))
+    out["hipblaslt_f32out_ms"] = t
+    out["hipblaslt_f32out_tflops"] = flop / t / 1e9
+    del lg
+    lg = torch.empty((B, N), dtype=torch.bfloat16, device=dev)
+    t = timeit(lambda: torch.mm(hb, wb.t(), out=lg))
+    out["hipblaslt_bf16out_ms"] = t
+    out["hipblaslt_bf16out_tflops"] = flop / t / 1e9
+    del lg
+    torch.cuda.empty_cache()
     t = timeit(lambda: H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act))
     out["fused_fwd_ms"] = t
     out["fused_fwd_tflops"] = flop / t / 1e9

@@ -9,5 +9,6 @@ FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-ma
 mkdir -p build/variants
 /opt/rocm/bin/hipcc $FLAGS "$@" -c -o build/variants/$N.o csrc/vmp_kernels.hip
 /opt/rocm/bin/hipcc $FLAGS -shared -o build/variants/libvmp_$N.so build/variants/$N.o \
-  build/obj/vmp_policy.hip.o build/obj/vmp_headgemm.hip.o build/obj/vmp_record.hip.o build/obj/vmp_capi.cpp.o
+  build/obj/vmp_policy.hip.o build/obj/vmp_headgemm.hip.o build/obj/vmp_headgemm_bf16.hip.o \
+  build/obj/vmp_record.hip.o build/obj/vmp_capi.cpp.o
 rm -f build/variants/$N.o

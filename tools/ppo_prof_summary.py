@@ -30,6 +30,8 @@ def kclass(name):
         return "head forward (HIP)"
     if "k_head_bwd" in name:
         return "head backward (HIP)"
+    if "k_hg16" in name:
+        return "fused bf16 GEMM + head, training (HIP)"
     if "k_head_gemm" in name or "k_hg_" in name:
         return "fused GEMM + head (HIP)"
     if "k_env" in name:
@@ -41,7 +43,7 @@ def kclass(name):
 
 def main():
     d = sys.argv[1]
-    for prec in ("f32", "bf16"):
+    for prec in sys.argv[2:] or ("f32", "bf16"):
         out = {}
         st = os.path.join(d, f"kt_{prec}", "run_kernel_stats.csv")
         if os.path.exists(st):

@@ -51,6 +51,8 @@ namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kBM = 256;       // samples per M block (NW waves x MC 16-sample columns)
 constexpr int kBK = 64;        // K per LDS stage
@@ -117,24 +119,25 @@ __device__ __forceinline__ float xmax(float v) {
   return fmaxf(v, __shfl_xor(v, 32));
 }
 
-// the row's mask words (bit j of word j >> 5 = action j invalid), bits past A cleared
+// the row's mask words (bit j of word j >> 5 = action j invalid), bits past A
+// cleared; W32 = ceil(A / 32) words per (sample, VM) row
+template <int W32>
 __device__ __forceinline__ void load_mask(const H16Args &a, int64_t row, uint32_t (&mw)[4]) {
   mw[0] = mw[1] = mw[2] = mw[3] = 0u;
   if (!a.bits) return;
-  const uint32_t *src = a.bits + row * a.W32;
-  if (a.W32 == 4) {
-    const uint4 v = *reinterpret_cast<const uint4 *>(src);
-    mw[0] = v.x, mw[1] = v.y, mw[2] = v.z, mw[3] = v.w;
+  const uint32_t *src = a.bits + row * W32;
+  if (W32 == 4) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(src);
+    mw[0] = v[0], mw[1] = v[1], mw[2] = v[2], mw[3] = v[3];
+  } else if (W32 == 2) {
+    const u32x2 v = *reinterpret_cast<const u32x2 *>(src);
+    mw[0] = v[0], mw[1] = v[1];
   } else {
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-      if (i < a.W32) mw[i] = src[i];
+    for (int i = 0; i < W32; i++) mw[i] = src[i];
   }
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int tail = a.A - 32 * i;
-    mw[i] &= tail >= 32 ? ~0u : (tail > 0 ? (1u << tail) - 1u : 0u);
-  }
+  const int tail = a.A - 32 * (W32 - 1);  // 1..32 bits in the last word
+  mw[W32 - 1] &= tail >= 32 ? ~0u : (1u << tail) - 1u;
 }
 
 // NW waves per workgroup, each owning MC = 16 / NW columns of 16 samples
@@ -142,6 +145,7 @@ __device__ __forceinline__ void load_mask(const H16Args &a, int64_t row, uint32_
 template <int TS, bool BWD, int NW>
 __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
+  constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
   constexpr int MC = 16 / NW, kThreads = 64 * NW;
   constexpr int kStageW = BNp * kRow, kStage = kStageW + kBM * kRow;
   extern __shared__ __align__(16) char lds_raw[];
@@ -187,6 +191,28 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
         bf16x8 hf[MC];
 #pragma unroll
         for (int mc = 0; mc < MC; mc++) hf[mc] = frag(Hs, 16 * (MC * wid + mc) + c, cl);
+#if defined(VMP_HG16_HOIST)
+        // the W fragments of VMP_HG16_HOIST tiles are read ahead of their MFMAs,
+        // pinned by a scheduling barrier (left alone, the compiler reads one
+        // fragment, waits for it, and issues its two MFMAs: every LDS latency
+        // exposed)
+        constexpr int G = VMP_HG16_HOIST;
+#pragma unroll
+        for (int n0 = 0; n0 < NT; n0 += G) {
+          bf16x8 wf[G];
+#pragma unroll
+          for (int i = 0; i < G; i++)
+            if (n0 + i < NT) wf[i] = frag(cur, 16 * (n0 + i) + c, cl);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < G; i++)
+            if (n0 + i < NT)
+#pragma unroll
+              for (int mc = 0; mc < MC; mc++)
+                acc[n0 + i][mc] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], hf[mc], acc[n0 + i][mc], 0, 0, 0);
+        }
+#else
 #pragma unroll
         for (int nt = 0; nt < NT; nt++) {
           const bf16x8 wf = frag(cur, 16 * nt + c, cl);
@@ -194,11 +220,19 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
           for (int mc = 0; mc < MC; mc++)
             acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hf[mc], acc[nt][mc], 0, 0, 0);
         }
+#endif
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
 
+#ifdef VMP_HG16_GEMM_ONLY  // timing-only build: the main loop alone (outputs wrong)
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+      for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
+    continue;
+#endif
     // ---- epilogue: per sample column mc, per segment s, in registers ----
 #pragma unroll
     for (int mc = 0; mc < MC; mc++) {
@@ -216,7 +250,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
         if (v >= a.V) break;  // workgroup-uniform: the last tile's missing segments
         const int64_t row = (int64_t)mm * a.V + v;
         uint32_t mw[4];
-        load_mask(a, row, mw);
+        load_mask<W32>(a, row, mw);
         const int act = a.action[row];
         const int tgt = (act >= 0 && act < a.A) ? act : -1;
         // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
@@ -230,7 +264,8 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
           for (int r = 0; r < 4; r++) {
             const int j = 16 * u + 4 * q + r;
             const float x = ((nib[u] >> r) & 1u) ? kMasked : acc[s * TS + u][mc][r];
-            xm[u][r] = j < a.A ? x : kPad;
+            // TS = ceil(A / 16): only the segment's last tile reaches past A
+            xm[u][r] = (u < TS - 1 || j < a.A) ? x : kPad;
             mx = fmaxf(mx, xm[u][r]);
           }
         }
@@ -238,7 +273,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
         // pass 2: p = exp(x - m) (x - m first: exact at x = m, so an all-masked
         // row gets p = 1 everywhere, as the unfused head), S, T = sum p x
         float p[TS][4];
-        float Ss = 0.f, Ts = 0.f, xa = 0.f;
+        float Ss = 0.f, Ts = 0.f;
 #pragma unroll
         for (int u = 0; u < TS; u++)
 #pragma unroll
@@ -246,8 +281,18 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
             p[u][r] = __builtin_amdgcn_exp2f((xm[u][r] - mx) * kLog2e);
             Ss += p[u][r];
             Ts = __builtin_fmaf(p[u][r], xm[u][r], Ts);
-            if (!BWD) xa = (16 * u + 4 * q + r == tgt) ? xm[u][r] : xa;
           }
+        float xa = 0.f;
+        if (!BWD) {  // the given action's logit: tile u_t, register r_t of lane q_t
+          const int ut = tgt >> 4, rt = tgt & 3, qt = (tgt >> 2) & 3;
+          float sel[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int u = 0; u < TS; u++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) sel[r] = u == ut ? xm[u][r] : sel[r];
+          xa = rt == 0 ? sel[0] : rt == 1 ? sel[1] : rt == 2 ? sel[2] : sel[3];
+          xa = (tgt >= 0 && q == qt) ? xa : 0.f;
+        }
         Ss = xsum(Ss);
         Ts = xsum(Ts);
         const float lse = mx + logf(Ss);
@@ -261,6 +306,13 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
           }
         } else {
           const float c1 = glp + gen * (H - lse);
+          // pass 1's per-element mask compares are recomputed from the nibbles
+          // here (kept live across pass 2 they are 64-bit SGPR pairs each, and
+          // spilled)
+#pragma unroll
+          for (int u = 0; u < TS; u++) asm volatile("" : "+v"(nib[u]));
+          int tq = tgt - 4 * q;
+          asm volatile("" : "+v"(tq));
 #pragma unroll
           for (int u = 0; u < TS; u++) {
             float d[4];
@@ -268,25 +320,27 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
             for (int r = 0; r < 4; r++) {
               const int j = 16 * u + 4 * q + r;
               float dd = -(p[u][r] * inv) * __builtin_fmaf(gen, xm[u][r], c1);
-              dd += (j == tgt) ? glp : 0.f;
+              dd += (16 * u + r == tq) ? glp : 0.f;
               d[r] = (j < a.A && !((nib[u] >> r) & 1u)) ? dd : 0.f;
             }
             // bf16 dlogits (round to nearest even), columns v A + j of row m
             const int j0 = 16 * u + 4 * q;
-            if (live && j0 < a.A) {
-              uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
-              const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
-              const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
-              const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
-              if (((a.A | a.ld) & 1) == 0 && j0 + 3 < a.A) {  // two 4-B stores
+            const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
+            const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
+            const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
+            uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
+            if (u < TS - 1 && ((a.A | a.ld) & 1) == 0) {
+              // the segment's inner tiles hold only real columns (TS = ceil(A / 16)):
+              // the lane's one condition is its sample
+              if (live) {
                 *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
                 *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
-              } else {
-                dst[0] = u0;
-                if (j0 + 1 < a.A) dst[1] = u1;
-                if (j0 + 2 < a.A) dst[2] = u2;
-                if (j0 + 3 < a.A) dst[3] = u3;
               }
+            } else if (live && j0 < a.A) {
+              dst[0] = u0;
+              if (j0 + 1 < a.A) dst[1] = u1;
+              if (j0 + 2 < a.A) dst[2] = u2;
+              if (j0 + 3 < a.A) dst[3] = u3;
             }
           }
         }
@@ -300,13 +354,7 @@ constexpr size_t lds_bytes() {
   return 2 * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow + 16 * (kMaxNT / TS * TS) * sizeof(float);
 }
 
-int pick_ts(int A) {  // the smallest built segment width (16 TS columns) that holds A
-  if (A <= 16) return 1;
-  if (A <= 32) return 2;
-  if (A <= 64) return 4;
-  if (A <= 112) return 7;
-  return 8;
-}
+int pick_ts(int A) { return (A + 15) / 16; }  // segment width: 16 TS columns, TS = ceil(A / 16)
 
 // M groups: the grid is n_tiles x m_groups workgroups at one per CU; pick the
 // group count whose last dispatch round is fullest (ties: fewer workgroups)
@@ -330,11 +378,12 @@ template <bool BWD, int NW>
 hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
   const dim3 grid((unsigned)((int64_t)a.n_tiles * a.m_groups)), block(64 * NW);
   switch (TS) {
-    case 1: hipLaunchKernelGGL((k_hg16<1, BWD, NW>), grid, block, lds_bytes<1>(), st, a); break;
-    case 2: hipLaunchKernelGGL((k_hg16<2, BWD, NW>), grid, block, lds_bytes<2>(), st, a); break;
-    case 4: hipLaunchKernelGGL((k_hg16<4, BWD, NW>), grid, block, lds_bytes<4>(), st, a); break;
-    case 7: hipLaunchKernelGGL((k_hg16<7, BWD, NW>), grid, block, lds_bytes<7>(), st, a); break;
+#define VMP_HG16_CASE(T) \
+  case T: hipLaunchKernelGGL((k_hg16<T, BWD, NW>), grid, block, lds_bytes<T>(), st, a); break;
+    VMP_HG16_CASE(1) VMP_HG16_CASE(2) VMP_HG16_CASE(3) VMP_HG16_CASE(4)
+    VMP_HG16_CASE(5) VMP_HG16_CASE(6) VMP_HG16_CASE(7)
     default: hipLaunchKernelGGL((k_hg16<8, BWD, NW>), grid, block, lds_bytes<8>(), st, a); break;
+#undef VMP_HG16_CASE
   }
   return hipGetLastError();
 }

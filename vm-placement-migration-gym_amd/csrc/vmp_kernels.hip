@@ -2252,6 +2252,7 @@ struct BigShared {
   double half[20];    // big_sum_phase: the two halves of a split job j at 2j, 2j + 1
   uint32_t fmax[kBigMaxWaves][128];  // big_heuristic: any-fit table per PM chunk
   int32_t wmin[kBigMaxWaves];         // block_min_1b
+  int32_t klflag[2];                  // big_kl_sums: means of jobs 2 / 3 published
 };
 
 // Rank of this thread's flag among the flagged threads of the block
@@ -2829,6 +2830,53 @@ __device__ __forceinline__ void big_sum_phase(const EnvParams &p, const Tables &
   if (split && block_combine) __syncthreads();
 }
 
+// kl's ten sums on the block's four waves with no barrier between a plain sum
+// and the squared deviations that need its mean: each wave runs the chain
+// whose mean it computes itself (PM sums 4 -> 6 on wave 0, 5 -> 7 on wave 1,
+// existing-VM sums 2 -> 8 on wave 2, 3 -> 9 on wave 3; the accepted sizes 0 /
+// 1 on waves 0 / 1), and a VM-size job past one pass (n_ex > kBigSplitMin) is
+// split at numpy's top level with its second half on wave 0 / 1 once wave 2 /
+// 3 has published the mean (LDS flag). Same jobs, same order of additions as
+// big_sum_phase: three passes on the longest wave instead of four.
+__device__ __forceinline__ void big_kl_sums(const EnvParams &p, const Tables &T, char LDSP *base,
+                                            BigShared &B, int k, int n_ex, uint32_t spill,
+                                            int mark) {
+  const int wid = threadIdx.x >> 6, lane = lane_id();
+  double LDSP *res = reinterpret_cast<double LDSP *>(base + p.off_stage);  // L.jobres
+  const bool split = n_ex > kBigSplitMin;
+  const int n2 = (n_ex / 2) - (n_ex / 2) % 8;
+  if (wid <= 1) {
+    const int j = wid;  // 0 / 1: accepted sizes, then PM sums 4 / 5 and their squares 6 / 7
+    if (k > 0) big_sum_job(p, T, base, j, n_ex, 0, k, res + j, spill);
+    big_sum_job(p, T, base, 4 + j, n_ex, 0, p.P, res + 4 + j, spill);
+    big_sum_job(p, T, base, 6 + j, n_ex, 0, p.P, res + 6 + j, spill);
+    if (split) {
+      while (__hip_atomic_load(&B.klflag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != mark)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      big_sum_job(p, T, base, 8 + j, n_ex, n2, n_ex - n2, (double LDSP *)&B.half[2 * (8 + j) + 1],
+                  spill);
+    }
+  } else if (wid <= 3) {
+    const int j = wid - 2;  // existing-VM sums 2 / 3, then their squared deviations 8 / 9
+    big_sum_job(p, T, base, 2 + j, n_ex, 0, n_ex, res + 2 + j, spill);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&B.klflag[j], mark, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (split)
+      big_sum_job(p, T, base, 8 + j, n_ex, 0, n2, (double LDSP *)&B.half[2 * (8 + j)], spill);
+    else
+      big_sum_job(p, T, base, 8 + j, n_ex, 0, n_ex, res + 8 + j, spill);
+  }
+  __syncthreads();
+  if (split && wid == 0) {
+    if (lane == 0) {
+      res[8] = B.half[16] + B.half[17];
+      res[9] = B.half[18] + B.half[19];
+    }
+    wsync();
+  }
+}
+
 // Wave 0 of k_env_big after the sums: reward, counters and termination.
 __device__ VMP_BIG_CALL void big_stats_final(const EnvParams &p, BigShared &B, char LDSP *base,
                                              int64_t k, int n_ex, int n_w, int64_t n_term,
@@ -3228,6 +3276,14 @@ VMP_SLOOP
 #ifdef VMP_WGTIME
     STAMP(17);  // wave 0: obs issued
 #endif
+#if !defined(VMP_ABL_NOA) && !defined(VMP_ABL_NOB) && !defined(VMP_KL_PHASES)
+    if (kl && kBigNT == 256) {  // kl on four waves: chained, no phase barrier
+      big_kl_sums(p, T, L.base, B, (int)k, n_ex, spill, kstep + 1);
+      STAMP(20);
+      STAMP(21);
+    } else
+#endif
+    {
 #ifndef VMP_ABL_NOA  // timing ablations only (rewards wrong): -DVMP_ABL_NOA / -DVMP_ABL_NOB
     if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, kBigSplitA, true, spill);
 #else
@@ -3238,6 +3294,7 @@ VMP_SLOOP
     if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true, false, spill);
 #endif
     STAMP(21);
+    }
   }
   if (w0) big_stats_final(p, B, L.base, k, n_ex, n_w, n_term, arrivals);
   __syncthreads();
@@ -3319,6 +3376,7 @@ __global__ __launch_bounds__(kBigNT, ONE ? VMP_BIG_WPE_ONE : 2) void k_env_big(E
   for (int i = 4 * NT + t; i < n_pm; i += NT) L.cpu[i] = pm[i];  // P > 2 * NT
   for (int i = t; i < (n_pm + 63) / 64; i += NT) L.pdirty[i] = 0;
   for (int i = t; i < kBigMaxSPT * kBigMaxWaves; i += NT) B.rc[i] = 0;
+  if (t < 2) B.klflag[t] = 0;
   __syncthreads();
   STAMP(13);
   bool term = false;
