@@ -475,3 +475,23 @@ def test_nominal_load_extra_null_slots_do_not_change_the_trajectory():
     assert torch.equal(pl3, pl10[:, :300]) and bool((pl10[:, 300:] == 101).all())
     for e in envs.values():
         e.close()
+
+
+def test_unknown_reward_function_asserts_at_first_rewarded_step():
+    """env.py:123-156: an unknown reward_function is only reached (assert
+    False, 'Function does not exist') once a step has VMs to reward; VmEnv
+    constructs, resets and steps with reward 0 until then."""
+    from vmp.config import Config
+    from vmp.env import VmEnv
+    cfg = Config(pms=10, vms=30, arrival_rate=0.05, service_length=20, training_steps=100,
+                 eval_steps=100, seed=3, reward_function="nope", allow_null_action=True)
+    env = VmEnv(cfg, device=DEV)
+    obs, _ = env.reset(seed=3)
+    quiet = 0
+    with pytest.raises(AssertionError, match="Function does not exist: nope"):
+        for _ in range(200):
+            obs, r, _, _, _ = env.step(obs[:cfg.vms].astype(np.int64))
+            assert r == 0.0
+            quiet += 1
+    assert quiet >= 1  # arrivals at rate 0.05: the first steps have no VM
+    env.close()

@@ -3277,7 +3277,13 @@ VMP_SLOOP
     STAMP(17);  // wave 0: obs issued
 #endif
 #if !defined(VMP_ABL_NOA) && !defined(VMP_ABL_NOB) && !defined(VMP_KL_PHASES)
-    if (kl && kBigNT == 256) {  // kl on four waves: chained, no phase barrier
+    // kl on four waves: chained, no phase barrier. Only wave 0 owns the LDS
+    // plan of the deep pairwise sums, so the chains need every job of waves
+    // 1-3 within the register plan (n <= pw_reg_cap): at P1000 / V10000
+    // under 2 000 arrivals per step n_ex reaches ~10 000 and the block falls
+    // back to the two phases (big_sum_phase sends those jobs to wave 0)
+    constexpr int kCap = pw_reg_cap(kBigPwDepth);
+    if (kl && kBigNT == 256 && n_ex <= kCap && (int)k <= kCap && p.P <= kCap) {
       big_kl_sums(p, T, L.base, B, (int)k, n_ex, spill, kstep + 1);
       STAMP(20);
       STAMP(21);

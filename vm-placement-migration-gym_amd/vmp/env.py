@@ -3,6 +3,7 @@ backed by one env of a BatchedVmEnv on the GPU. Numpy in, numpy out, same
 observation / action / reward / info contract, so the reference agents and
 drivers (main.py, src/agents/*) can use it unchanged.
 """
+import copy
 from typing import Optional
 
 import numpy as np
@@ -53,7 +54,17 @@ class VmEnv(_GymEnv):
         self.action_space = _multidiscrete(np.full(config.vms, self.action_dim))
         self.WAIT_STATUS = config.pms
         self.NULL_STATUS = config.pms + 1
-        self._b = BatchedVmEnv(config, 1, seeds=[int(config.seed)], device=device)
+        # an unknown reward_function fails where the reference's does: at the
+        # first step that has VMs to reward (env.py:123-156 asserts in the
+        # reward's else branch); until then the env runs (reward 0, no VMs)
+        from ._lib import REWARDS
+        self._bad_reward = None
+        cfg = config
+        if getattr(config, "reward_function", None) not in REWARDS:
+            self._bad_reward = getattr(config, "reward_function", None)
+            cfg = copy.copy(config)
+            cfg.reward_function = "wr"
+        self._b = BatchedVmEnv(cfg, 1, seeds=[int(config.seed)], device=device)
         self.reset(config.seed)
 
     # ------------------------------------------------------- state views
@@ -117,6 +128,8 @@ class VmEnv(_GymEnv):
         obs, reward, done, valid = self._b.step(a)
         ts_before = self.timestep - 1
         obs = obs[0].cpu().numpy()
+        if self._bad_reward is not None and np.any(obs[:self.config.vms] <= self.WAIT_STATUS):
+            raise AssertionError(f"Function does not exist: {self._bad_reward}")
         # zeros_like(action) in the reference (env.py:68)
         valid = valid[0].cpu().numpy().astype(action.dtype if action.dtype.kind in "iu" else np.int64)
         info = {}
