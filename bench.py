@@ -79,6 +79,10 @@ def main():
     ap.add_argument("--period-steps", type=int, default=1000,
                     help="period leg: consecutive launches of phase-aligned envs (0: skip)")
     ap.add_argument("--period-ff", type=int, default=2000)
+    ap.add_argument("--period-groups", type=int, default=1,
+                    help="period leg phase groups (1: phase-aligned; > 1: staggered as "
+                         "the headline, --phase-delta apart, to price the mixing itself)")
+    ap.add_argument("--period-dump", default="", help="period leg: save the per-launch ms (.npy)")
     ap.add_argument("--period-only", action="store_true",
                     help="run only the period leg (rocprofv3 of that window)")
     ap.add_argument("--nominal-steps", type=int, default=50,
@@ -353,7 +357,11 @@ def bench_period(args, dev, rank, world, dist, cfg):
     P, V = cfg["pms"], cfg["vms"]
     env = BatchedVmEnv(Config(**cfg), N, seeds=shard_seeds(rank, N), device=dev)
     env.eval(False)
-    left = args.period_ff
+    G = max(1, args.period_groups)
+    if G > 1:  # same window position, envs' ages spread as in the headline leg
+        fast_forward(env, "firstfit", shard_seeds(rank, N), args.period_ff - (G - 1) * args.phase_delta,
+                     G, args.phase_delta, args.rollout_k)
+    left = args.period_ff if G == 1 else 0
     while left > 0:
         env.rollout("firstfit", min(args.rollout_k, left))
         left -= args.rollout_k
@@ -383,6 +391,8 @@ def bench_period(args, dev, rank, world, dist, cfg):
     c1 = env.counters()
     words, pmw = changed_words(c0, c1, N * K)
     ms = np.array([a.elapsed_time(b) for a, b in ev])
+    if args.period_dump and rank == 0:
+        np.save(args.period_dump, ms)
     env.close()
     mean_ms = _max_over_ranks(float(ms.mean()), dev, dist)
     bins = [round(float(ms[i:i + 100].mean()), 4) for i in range(0, K, 100)]
@@ -391,7 +401,9 @@ def bench_period(args, dev, rank, world, dist, cfg):
     return {"value": world * N / (mean_ms * 1e-3), "unit": "env-steps/s",
             "value_kind": "mean per-launch kernel time over the window",
             "wall_value": world * N * K / el,
-            "window": f"steps {args.period_ff + 1}-{args.period_ff + K} of phase-aligned envs",
+            "window": f"steps {args.period_ff + 1}-{args.period_ff + K} of "
+                      + ("phase-aligned envs" if G == 1 else
+                         f"envs in {G} phase groups {args.phase_delta} steps apart"),
             "steps": K, "mean_ms": mean_ms, "max_ms": float(ms.max()),
             "min_ms": float(ms.min()), "ms_by_100_steps": bins,
             "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,

@@ -169,8 +169,9 @@ def rollout(cfg: dict, n_env, seed0, stride, steps, policy=0, eval_mode=True, th
 def rollout_timed(cfg: dict, n_env, seed0, stride, warmup, steps, policy=0, threads=1,
                   eval_mode=False, reps=1):
     """Warm-started timed CPU rollout (bench.py cpu_baseline): `reps` timed
-    passes of `steps` steps over the same envs. Returns (seconds[reps],
-    reward_sum[reps, n_env])."""
+    passes of `steps` steps over the same window (the envs are restored to
+    their post-warm-up state before every pass, untimed), so every pass does
+    identical work. Returns (seconds[reps], reward_sum[reps, n_env])."""
     c = make_config(cfg)
     rs = np.zeros((reps, n_env))
     secs = np.zeros(reps)

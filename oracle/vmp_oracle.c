@@ -774,10 +774,40 @@ int64_t oracle_rollout(const vmp_config *cfg, int32_t n_env, int64_t seed0, int6
 // timed passes of `steps` act+step each (secs[r] = wall seconds of pass r).
 // Envs are dealt to threads in contiguous blocks (schedule static), each
 // thread keeping its own envs across the passes.
+/* d := s (same config): the state VmEnv.step reads and writes; d keeps its
+   own buffers (the scratch arrays are not state) */
+static void oenv_assign(oenv *d, const oenv *s) {
+  int V = s->V, P = s->P;
+  memcpy(d->placement, s->placement, sizeof(int64_t) * V);
+  memcpy(d->remaining, s->remaining, sizeof(int64_t) * V);
+  memcpy(d->vm_cpu, s->vm_cpu, sizeof(double) * V);
+  memcpy(d->vm_mem, s->vm_mem, sizeof(double) * V);
+  memcpy(d->cpu, s->cpu, sizeof(double) * P);
+  memcpy(d->mem, s->mem, sizeof(double) * P);
+  d->eval_mode = s->eval_mode;
+  d->timestep = s->timestep;
+  d->total_requests = s->total_requests;
+  d->served = s->served;
+  d->suspend_action = s->suspend_action;
+  d->place_action = s->place_action;
+  d->dropped = s->dropped;
+  d->total_cpu_req = s->total_cpu_req;
+  d->total_mem_req = s->total_mem_req;
+  d->waiting_ratio = s->waiting_ratio;
+  d->tcm = s->tcm;
+  d->tmm = s->tmm;
+  memcpy(d->rng, s->rng, sizeof(s->rng));
+  memcpy(d->seq_base, s->seq_base, sizeof(s->seq_base));
+}
+
+/* CPU baseline timing: every pass steps the SAME window (the envs are
+   restored to their post-warm-up state before each pass, outside the timed
+   region), so the passes' spread is timing noise, not workload drift. */
 void oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0, int64_t stride,
                           int64_t warmup, int64_t steps, int32_t policy, int32_t n_threads,
                           int32_t eval_mode, int32_t reps, double *secs, double *reward_sum) {
   oenv **envs = (oenv **)calloc(n_env, sizeof(oenv *));
+  oenv **snap = (oenv **)calloc(n_env, sizeof(oenv *));
   double tstart = 0.0;  // shared: set by one thread per pass
 #pragma omp parallel num_threads(n_threads)
   {
@@ -795,8 +825,16 @@ void oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0, i
         int term;
         oracle_step(envs[i], act, NULL, &r, &term);
       }
+      if (reps > 1) {
+        snap[i] = oracle_create(&c);
+        oenv_assign(snap[i], envs[i]);
+      }
     }
     for (int32_t rep = 0; rep < reps; rep++) {
+      if (rep > 0) {
+#pragma omp for schedule(static)
+        for (int32_t i = 0; i < n_env; i++) oenv_assign(envs[i], snap[i]);
+      }
 #pragma omp single
       tstart = omp_get_wtime();  // the single's implicit barrier publishes it
 #pragma omp for schedule(static)
@@ -818,6 +856,10 @@ void oracle_rollout_timed(const vmp_config *cfg, int32_t n_env, int64_t seed0, i
     }
     free(act);
   }
-  for (int32_t i = 0; i < n_env; i++) oracle_destroy(envs[i]);
+  for (int32_t i = 0; i < n_env; i++) {
+    oracle_destroy(envs[i]);
+    oracle_destroy(snap[i]);
+  }
   free(envs);
+  free(snap);
 }

@@ -159,3 +159,22 @@ def test_published_exp_suspension_rows(row):
                arrival_rate=float(np.round(100 / 0.55 / L * load, 3)))
     _, ctr = O.rollout(cfg, 1, 0, 1, 100000, policy=0 if agent == "firstfit" else 1)
     assert ctr[0, 1] == served and ctr[0, 2] == susp and ctr[0, 2] + ctr[0, 3] == valid, ctr[0]
+
+
+def test_rollout_timed_passes_repeat_the_same_window():
+    """bench.py cpu_baseline: every timed pass restarts from the post-warm-up
+    state, so the passes do identical work (same per-env reward sums), and
+    they equal a plain OracleEnv FirstFit rollout of the same seeds."""
+    cfg = dict(pms=10, vms=30, arrival_rate=0.3, service_length=20, reward_function="wr")
+    secs, rs = O.rollout_timed(cfg, 4, 7, 3, 25, 40, 0, 2, reps=3)
+    assert secs.shape == (3,) and (secs > 0).all()
+    np.testing.assert_array_equal(rs[0], rs[1])
+    np.testing.assert_array_equal(rs[0], rs[2])
+    for i in range(4):
+        e = O.OracleEnv(dict(cfg, seed=7 + 3 * i))
+        tot = 0.0
+        for s in range(65):
+            _, r, _, _ = e.step(e.firstfit())
+            if s >= 25:
+                tot += r
+        assert tot == rs[0, i]

@@ -53,6 +53,25 @@ def main():
     flop = 2.0 * B * K * N
     out = {"B": B, "K": K, "V": V, "A": A}
 
+    if os.environ.get("GEMM_AB") == "1":  # the backward's dh / dW GEMM layouts (hipBLASLt)
+        r = min(B, 70144)
+        d = (torch.randn((r, N), device=dev, generator=g) * 1e-3).bfloat16()
+        wbT = wb.t().contiguous()                       # [K, N]
+        haug = torch.zeros((r, K + 8), dtype=torch.bfloat16, device=dev)
+        haug[:, :K] = hb[:r]
+        haug[:, K] = 1
+        f = 2.0 * r * N * K
+        res = {}
+        for name, fn in (("dh d@W [N,K] row-major", lambda: torch.mm(d, wb, out_dtype=torch.float32)),
+                         ("dh d@(W^T)^T", lambda: torch.mm(d, wbT.t(), out_dtype=torch.float32)),
+                         ("dh (W^T @ d^T)^T", lambda: torch.mm(wbT, d.t(), out_dtype=torch.float32)),
+                         ("dW d^T@[h|1]", lambda: torch.mm(d.t(), haug, out_dtype=torch.float32)),
+                         ("dW d^T@h", lambda: torch.mm(d.t(), hb[:r], out_dtype=torch.float32)),
+                         ("dW ([h|1]^T@d)^T", lambda: torch.mm(haug.t(), d, out_dtype=torch.float32))):
+            t = timeit(fn, n=10)
+            res[name] = {"ms": round(t, 3), "tflops": round(f / t / 1e9, 1)}
+        print(json.dumps(res), flush=True)
+        return
     if os.environ.get("FWD_ONLY") == "1":  # variant A/B: the fused kernels alone
         t = timeit(lambda: H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act), n=10)
         r = min(B, 70144)
