@@ -17,7 +17,7 @@ K = int(os.environ.get("PROF_STEPS", "20"))
 cfg = Config(pms=100, vms=1000, arrival_rate=1.8182, service_length=1000, training_steps=10000,
              eval_steps=100000, seed=0, reward_function="wr", allow_null_action=True)
 env = BatchedVmEnv(cfg, N, seeds=4 * np.arange(N, dtype=np.int64))
-env.eval(True)
+env.eval(os.environ.get("PROF_EVAL", "1") == "1")  # bench.py: PROF_EVAL=0 (training)
 for _ in range(25):
     env.rollout("firstfit", 100)
 D = 3 * 1000 + 200

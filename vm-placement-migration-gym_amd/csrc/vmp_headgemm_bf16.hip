@@ -61,6 +61,9 @@ constexpr int kMaxNT = 14;     // 16-column accumulator tiles per workgroup
 constexpr float kMasked = -1e7f;   // ppo.py:119
 constexpr float kPad = -1e30f;     // tile columns past A: p = 0, never the max
 constexpr float kLog2e = 1.44269504088896341f;
+#ifndef VMP_HG16_PIPE
+#define VMP_HG16_PIPE 4  // W fragments in flight ahead of their MFMAs
+#endif
 
 struct H16Args {
   int B, K, V, A, W32, n_tiles, m_blocks, m_groups, ld;
@@ -164,10 +167,27 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   __syncthreads();
 
   const int nk = a.K / kBK;
+  // VMP_HG16_PRE: the epilogue's mask words and actions are loaded during the
+  // last K stage (their latency under its MFMAs)
+#ifdef VMP_HG16_PRE  // measured: +1 ms on the V300 forward (register pressure), off
+  constexpr bool kPre = MC * S * (W32 + 1) <= (BWD ? 12 : 20);
+#else
+  constexpr bool kPre = false;
+#endif
+  constexpr int kPS = kPre ? S : 1;
+  uint32_t pmw[MC][kPS][4];
+  int pact[MC][kPS];
 
+  int sb = 0;  // LDS stage of K step 0 of this M block
+  // K step 0 of the first M block; later blocks' step 0 is issued during the
+  // previous block's last K step, into the stage that step does not read
+  stage_issue<TS, NT, NW>(a, lds, v0, g * kBM, 0, wid, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 #pragma unroll 1
   for (int mb = g; mb < a.m_blocks; mb += a.m_groups) {
     const int m0 = mb * kBM;
+    const int mn = mb + a.m_groups;  // next M block of this workgroup
     f32x4 acc[NT][MC];
 #pragma unroll
     for (int nt = 0; nt < NT; nt++) {
@@ -176,15 +196,59 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
       for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
     }
     // ---- GEMM: two LDS stages, the next stage's DMA under this stage's MFMAs ----
-    stage_issue<TS, NT, NW>(a, lds, v0, m0, 0, wid, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
 #pragma unroll 1
     for (int s = 0; s < nk; s++) {
-      const char LDSP *cur = lds + (s & 1) * kStage;
-      if (s + 1 < nk)
-        stage_issue<TS, NT, NW>(a, lds + ((s + 1) & 1) * kStage, v0, m0, (s + 1) * kBK, wid, lane);
+      const char LDSP *cur = lds + ((sb + s) & 1) * kStage;
+      char LDSP *nxt = lds + ((sb + s + 1) & 1) * kStage;
+      if (s + 1 < nk) {
+        stage_issue<TS, NT, NW>(a, nxt, v0, m0, (s + 1) * kBK, wid, lane);
+      } else {
+        if (mn < a.m_blocks) stage_issue<TS, NT, NW>(a, nxt, v0, mn * kBM, 0, wid, lane);
+        if (kPre) {
+#pragma unroll
+          for (int mc = 0; mc < MC; mc++) {
+            const int m = m0 + 16 * (MC * wid + mc) + c;
+            const int64_t rb = (int64_t)(m < a.B ? m : a.B - 1) * a.V;
+#pragma unroll
+            for (int s2 = 0; s2 < kPS; s2++) {
+              const int64_t row = rb + min(v0 + s2, a.V - 1);
+              load_mask<W32>(a, row, pmw[mc][s2]);
+              pact[mc][s2] = a.action[row];
+            }
+          }
+        }
+      }
       const char LDSP *Hs = cur + kStageW;
+#if !defined(VMP_HG16_NOPIPE)
+      // the stage's 2 x NT W fragments are read kPipe ahead of their two MFMAs
+      // (an LDS read's latency is several 16-cycle MFMA pairs: read right
+      // before its use, every pair waited on it); both K halves' h fragments
+      // up front. The sched_group_barriers pin the pattern
+      // {MFMA, MFMA, ds_read} so the compiler does not sink the reads again.
+      constexpr int kPipe = VMP_HG16_PIPE, NF = 2 * NT;
+      bf16x8 hf[2][MC];
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+        for (int mc = 0; mc < MC; mc++) hf[kk][mc] = frag(Hs, 16 * (MC * wid + mc) + c, 4 * kk + q);
+      bf16x8 wf[kPipe];
+#pragma unroll
+      for (int i = 0; i < kPipe; i++) wf[i] = frag(cur, 16 * (i % NT) + c, 4 * (i / NT) + q);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * MC + kPipe, 0);
+#pragma unroll
+      for (int i = 0; i < NF; i++) {
+        const int kk = i / NT, nt = i % NT;
+#pragma unroll
+        for (int mc = 0; mc < MC; mc++)
+          acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i % kPipe], hf[kk][mc], acc[nt][mc], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MC, 0);
+        if (i + kPipe < NF) {
+          const int j = i + kPipe;
+          wf[i % kPipe] = frag(cur, 16 * (j % NT) + c, 4 * (j / NT) + q);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+#else
 #pragma unroll
       for (int kk = 0; kk < 2; kk++) {
         const int cl = 4 * kk + q;
@@ -222,9 +286,11 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
         }
 #endif
       }
+#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+    sb = (sb + nk) & 1;
 
 #ifdef VMP_HG16_GEMM_ONLY  // timing-only build: the main loop alone (outputs wrong)
 #pragma unroll
@@ -250,8 +316,15 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
         if (v >= a.V) break;  // workgroup-uniform: the last tile's missing segments
         const int64_t row = (int64_t)mm * a.V + v;
         uint32_t mw[4];
-        load_mask<W32>(a, row, mw);
-        const int act = a.action[row];
+        int act;
+        if (kPre) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) mw[i] = pmw[mc][s < kPS ? s : 0][i];
+          act = pact[mc][s < kPS ? s : 0];
+        } else {
+          load_mask<W32>(a, row, mw);
+          act = a.action[row];
+        }
         const int tgt = (act >= 0 && act < a.A) ? act : -1;
         // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
         float xm[TS][4];
