@@ -62,6 +62,18 @@ def main():
         haug[:, K] = 1
         f = 2.0 * r * N * K
         res = {}
+        for ka in (576, 640):  # [h | 1 | 0...] padded to a multiple of 64 / 128
+            hk = torch.zeros((r, ka), dtype=torch.bfloat16, device=dev)
+            hk[:, :K] = hb[:r]
+            hk[:, K] = 1
+            t = timeit(lambda: torch.mm(d.t(), hk, out_dtype=torch.float32), n=10)
+            res[f"dW d^T@[h|1] KA {ka}"] = {"ms": round(t, 3), "tflops": round(f / t / 1e9, 1)}
+            del hk
+        t = timeit(lambda: d.sum(0, dtype=torch.float32), n=10)
+        res["db d.sum(0, f32)"] = {"ms": round(t, 3), "GB/s": round(2.0 * r * N / t / 1e6, 1)}
+        ones = torch.ones((1, r), dtype=torch.bfloat16, device=dev)
+        t = timeit(lambda: torch.mm(ones, d, out_dtype=torch.float32), n=10)
+        res["db 1^T d"] = {"ms": round(t, 3), "GB/s": round(2.0 * r * N / t / 1e6, 1)}
         for name, fn in (("dh d@W [N,K] row-major", lambda: torch.mm(d, wb, out_dtype=torch.float32)),
                          ("dh d@(W^T)^T", lambda: torch.mm(d, wbT.t(), out_dtype=torch.float32)),
                          ("dh (W^T @ d^T)^T", lambda: torch.mm(wbT, d.t(), out_dtype=torch.float32)),

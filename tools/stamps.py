@@ -21,8 +21,13 @@ cfg = Config(pms=100, vms=V, arrival_rate=1.8182, service_length=1000, training_
 env = BatchedVmEnv(cfg, N)
 env.eval(os.environ.get("STAMP_TRAIN") is None)
 FF = int(sys.argv[3]) if len(sys.argv) > 3 else 2500
-for _ in range(FF // 100):
-    env.rollout("firstfit", 100)
+G = int(os.environ.get("STAMP_GROUPS", "1"))  # > 1: phases staggered as bench.py's headline
+if G > 1:
+    import bench  # noqa: E402
+    bench.fast_forward(env, "firstfit", 4 * np.arange(N, dtype=np.int64), FF - (G - 1) * 100, G, 100, 100)
+else:
+    for _ in range(FF // 100):
+        env.rollout("firstfit", 100)
 NS = 24
 buf = torch.zeros((N, NS), dtype=torch.int64, device="cuda")
 _lib.check(_lib.lib().vmp_debug_stamps(env._bind(), _lib.ptr(buf)))
@@ -55,3 +60,9 @@ cyc = st[:, 9]
 print(f"wave lifetime: {wall_us.mean():.1f} us wall (mean), {cyc.mean():.0f} shader cycles -> "
       f"{cyc.mean() / wall_us.mean() / 1e3:.2f} GHz")
 print("mean waiting", (pl == 100).sum(1).mean(), "running", (pl < 100).sum(1).mean())
+q = np.percentile(wall_us, [10, 50, 90, 99])
+print(f"wave lifetime percentiles (us): p10 {q[0]:.1f} p50 {q[1]:.1f} p90 {q[2]:.1f} p99 {q[3]:.1f} "
+      f"max {wall_us.max():.1f}")
+if G > 1:  # env i is in phase group i mod G (reset (i mod G) * 100 steps late)
+    for g in range(G):
+        print(f"  group {g} (age {FF - 100 * g}): lifetime {wall_us[g::G].mean():.1f} us")

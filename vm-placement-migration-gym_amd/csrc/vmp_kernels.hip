@@ -1198,7 +1198,7 @@ __device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, const 
   // skipped would come from svc_fallback, from the same stream position.
   const uint64_t hint = H->pad;
 #ifndef VMP_NO_DRAW_HINT
-  const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 0x7FFFFFFFu) == 0 &&
+  const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 0x3FFFFFFFu) == 0 &&
                          (uint32_t)hint > (uint32_t)H->timestep + 1u;
 #else  // A/B switch
   const bool none_free = false && hint;
@@ -1281,7 +1281,8 @@ template <int VPT>
 __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds &L,
                                                    const Tables &T, uint32_t (&wa)[VPT],
                                                    int policy, int32_t *act_out,
-                                                   uint8_t *valid_out STAMP_PARAMS) {
+                                                   uint8_t *valid_out, bool quiet,
+                                                   bool &fit_any STAMP_PARAMS) {
   const int lane = lane_id();
   const int P = p.P, WAIT = p.P;
   const bool bf = policy == 1;
@@ -1291,7 +1292,12 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     if (w_pl(wa[s]) == WAIT) pend |= 1u << s;
   uint32_t won = 0, bad = 0;
   int64_t n_place = 0;
-  if (ballot(pend != 0)) {
+  fit_any = false;
+  // quiet (EnvHdr::pad bit 62): the previous step found no pending VM that
+  // fits any PM, and since then no VM finished (no PM load fell) and none
+  // arrived (no new pending VM): nothing fits now either, so the heuristic
+  // places nothing and the any-fit table need not be built
+  if (!quiet && ballot(pend != 0)) {
     for (int i = lane; i < P; i += 64) {
       const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
       L.fcpu[i] = fcv;
@@ -1310,6 +1316,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     for (int s = 0; s < VPT; s++)
       hit |= (uint32_t)(((pend >> s) & 1u) && M[w_cc(wa[s])] > (uint32_t)w_cm(wa[s])) << s;
     const bool anyfit = ballot(hit != 0) != 0;
+    fit_any = anyfit;
     STAMP(17);
 #pragma unroll 1
     for (; anyfit;) {
@@ -1498,7 +1505,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
                                            uint32_t (&wa)[VPT], uint32_t (&rem)[VPT],
                                            uint32_t run0, uint32_t fb, uint32_t &dirty,
                                            uint64_t *vmo, int kstep,
-                                           bool &terminated STAMP_PARAMS) {
+                                           bool &terminated, bool &calm STAMP_PARAMS) {
   const int lane = lane_id();
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
   EnvHdr LDSP *H = L.hdr;
@@ -1697,6 +1704,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
   // ---- counters, termination (env.py:160-163, 101) ----
   const int64_t ts = H->timestep;
   terminated = ts >= p.limit;
+  calm = n_term == 0 && k == 0;  // no PM load fell, no new pending VM
   wsync();
   if (lane == 0) {
     H->timestep = ts + 1;
@@ -1893,6 +1901,9 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   }
   uint64_t *vmo = p.vmw + (int64_t)e * V;
   const int k_steps = ONE ? 1 : o.k_steps;
+  // EnvHdr::pad bit 62 (see heuristic_apply); the external-action kernel
+  // neither uses nor keeps it
+  bool quiet = !EXT && ((L.hdr->pad >> 62) & 1u);
 #pragma unroll 1
   for (int k = 0; k < k_steps; k++) {
     const bool last = k == k_steps - 1;
@@ -1902,8 +1913,10 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     uint32_t run0 = 0;
 #pragma unroll
     for (int s = 0; s < VPT; s++) run0 |= (uint32_t)(w_pl(wa[s]) < P) << s;
+    bool fit_any = false;
     if (!EXT)
-      n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row STAMP_ARGS);
+      n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row, quiet,
+                                     fit_any STAMP_ARGS);
     else {
       // the external kernel loads the time words after its action phase: live
       // across it beside the 16 action words they spilled 10 VGPRs
@@ -1943,7 +1956,10 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
       L.hdr->suspend_action += n_susp;
     }
     wsync();
-    const double r = env_tail<VPT, ONE>(p, L, T, wa, rem, run0, fb, dirty, vmo, k, term STAMP_ARGS);
+    bool calm = false;
+    const double r = env_tail<VPT, ONE>(p, L, T, wa, rem, run0, fb, dirty, vmo, k, term,
+                                        calm STAMP_ARGS);
+    quiet = !EXT && !fit_any && calm;
     if (o.reward && lane == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
@@ -1953,7 +1969,9 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     uint32_t wt[VPT];
 #pragma unroll
     for (int s = 0; s < VPT; s++) wt[s] = wa[s];
-    heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr STAMP_ARGS);
+    bool fit_any;
+    heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr, quiet,
+                         fit_any STAMP_ARGS);
   }
   STAMP(0);
   if (o.obs) write_obs<VPT>(p, L, T, wa, o.obs + (int64_t)e * p.D);
@@ -2000,6 +2018,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
         }
         hint = (1ull << 63) | ((uint64_t)nn << 32) | m;
       }
+      hint |= (uint64_t)quiet << 62;
       wsync();
       if (lane == 0) L.hdr->pad = hint;
       wsync();

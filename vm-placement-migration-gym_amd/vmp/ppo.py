@@ -184,9 +184,8 @@ class BF16FusedActorHead(torch.autograd.Function):
     bf16 matrix-core kernels (vmp_actor_head_bf16_fwd/_bwd):
     the forward consumes each logits tile in registers; the backward recomputes
     the tiles chunk by chunk (`chunk_rows` samples at a time) and writes only
-    that chunk's bf16 dlogits, which two GEMMs turn into dh and [dW | db] (the
-    bias gradient is the product with a column of ones appended to h). No
-    [B, V*A] tensor is allocated in either direction."""
+    that chunk's bf16 dlogits, which two GEMMs turn into dh and dW (and a
+    column sum into db). No [B, V*A] tensor is allocated in either direction."""
 
     @staticmethod
     def forward(ctx, x, w, b, bits, action, V, A, chunk_rows):
@@ -209,11 +208,12 @@ class BF16FusedActorHead(torch.autograd.Function):
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         dl = torch.empty((R, N), dtype=torch.bfloat16, device=dev)
         gx = torch.empty((B, K), dtype=torch.float32, device=dev) if need_x else None
-        # h | 1 | 0...: the dW GEMM's extra output column K is the bias gradient
-        KA = K + 8
-        haug = torch.zeros((R, KA), dtype=torch.bfloat16, device=dev)
-        haug[:, K] = 1.0
-        gwa = None
+        # dW = dlogits^T h and db = 1^T dlogits, per chunk. (The
+        # bias column appended to h, dlogits^T [h | 1 | 0...], falls off
+        # hipBLASLt's fast kernels: 3.7 ms vs 2.4 + 0.8 ms per 70 144-row chunk,
+        # profiles/r04_hg16_gemm_layouts.log.)
+        gw = gb = None
+        ones = torch.ones((1, R), dtype=torch.bfloat16, device=dev) if need_b else None
         for r0 in range(0, B, R):
             r1 = min(B, r0 + R)
             n = r1 - r0
@@ -222,13 +222,12 @@ class BF16FusedActorHead(torch.autograd.Function):
                                   act[r0:r1], glp[r0:r1], gen[r0:r1], d)
             if need_x:
                 gx[r0:r1] = torch.mm(d, wb, out_dtype=torch.float32)
-            if need_w or need_b:
-                ha = haug[:n]
-                ha[:, :K] = xb[r0:r1]
-                part = torch.mm(d.t(), ha, out_dtype=torch.float32)
-                gwa = part if gwa is None else gwa.add_(part)
-        gw = gwa[:, :K].contiguous() if need_w else None
-        gb = gwa[:, K].contiguous() if need_b else None
+            if need_w:
+                part = torch.mm(d.t(), xb[r0:r1], out_dtype=torch.float32)
+                gw = part if gw is None else gw.add_(part)
+            if need_b:  # (d.sum(0, dtype=float32) would allocate an f32 copy of d)
+                part = torch.mm(ones[:, :n], d, out_dtype=torch.float32)[0]
+                gb = part if gb is None else gb.add_(part)
         return gx, gw, gb, None, None, None, None, None
 
 
