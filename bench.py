@@ -255,7 +255,9 @@ def main():
                   "rewards_compared": len(errs)}
 
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(CFG, args.cpu_threads, "same config")
+            # 48 envs per thread: ~1.5 s passes (16 per thread gave ~0.5 s
+            # passes and up to 6 % spread under the box's CPU quota)
+            cpu = cpu_baseline(CFG, args.cpu_threads, "same config", envs_per_thread=48)
 
     bpe = step_bytes(P, V, words, pmw)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
@@ -466,7 +468,9 @@ def bench_nominal(args, dev, rank, world, dist):
     ach = bpe * N / (kern_ms * 1e-3) / 1e9
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(cfg, args.cpu_threads, "lambda 0.182")
+        # 160 envs per thread: a pass of ~1 s (16 envs per thread pass in
+        # ~0.1 s, where the cgroup's 100 ms CPU-quota periods make the spread)
+        cpu = cpu_baseline(cfg, args.cpu_threads, "lambda 0.182", envs_per_thread=160)
     return {"value": world * N * K / el, "unit": "env-steps/s", "dtype": "f64",
             "workload": "config/100.yml with vms=1000, lambda 0.182 (100 % load), L 1000, "
                         "reward wr, FirstFit act + step, one launch per step",
@@ -503,11 +507,12 @@ def host_cpus():
             "cpu_model": model}
 
 
-def cpu_baseline(cfg, threads=0, what=""):
+def cpu_baseline(cfg, threads=0, what="", envs_per_thread=16):
     """SURVEY §8(d) / BASELINE.md §4 CPU baseline: the C oracle (FirstFit act +
     VmEnv.step, training mode as the GPU leg) over OpenMP on every core this
     process may run on (the affinity set, capped by the cgroup's CPU quota when
-    one is set: threads beyond the quota only time-slice), 16 envs per thread,
+    one is set: threads beyond the quota only time-slice), 16 envs per thread
+    (envs_per_thread),
     warmed up 2 500 steps (the GPU window's env ages), then 3 timed passes of
     1 000 steps (one service period each); value = the median pass, spread =
     (max - min) / median."""
@@ -517,7 +522,7 @@ def cpu_baseline(cfg, threads=0, what=""):
         threads = host["affinity"]
         if host["cgroup_quota_cores"]:
             threads = max(1, min(threads, int(host["cgroup_quota_cores"])))
-    n_env, warm, steps, reps = 16 * threads, 2500, 1000, 3
+    n_env, warm, steps, reps = envs_per_thread * threads, 2500, 1000, 3
     secs, _ = O.rollout_timed(cfg, n_env, 0, 4, warm, steps, 0, threads, eval_mode=False,
                               reps=reps)
     rates = n_env * steps / secs

@@ -1198,7 +1198,7 @@ __device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, const 
   // skipped would come from svc_fallback, from the same stream position.
   const uint64_t hint = H->pad;
 #ifndef VMP_NO_DRAW_HINT
-  const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 0x3FFFFFFFu) == 0 &&
+  const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 0x1FFFFFFFu) == 0 &&
                          (uint32_t)hint > (uint32_t)H->timestep + 1u;
 #else  // A/B switch
   const bool none_free = false && hint;
@@ -1504,8 +1504,9 @@ template <int VPT, bool LAZY>
 __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, const Tables &T,
                                            uint32_t (&wa)[VPT], uint32_t (&rem)[VPT],
                                            uint32_t run0, uint32_t fb, uint32_t &dirty,
-                                           uint64_t *vmo, int kstep,
-                                           bool &terminated, bool &calm STAMP_PARAMS) {
+                                           uint64_t *vmo, int kstep, bool ext,
+                                           bool quiet_in, bool &terminated, bool &calm,
+                                           bool &has_ex STAMP_PARAMS) {
   const int lane = lane_id();
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
   EnvHdr LDSP *H = L.hdr;
@@ -1552,20 +1553,31 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
       dirty |= 1u << s;
     }
   }
-  for (int i = lane; i < P; i += 64) {  // precision clamp (env.py:267-268)
-    if (L.cpu[i] < 1e-7) L.cpu[i] = 0;
-    if (L.mem[i] < 1e-7) L.mem[i] = 0;
-  }
+  // precision clamp (env.py:267-268): every stored load is 0 or >= 1e-7 after
+  // the previous step's clamp and placements only add, so only a free or a
+  // suspension (external actions) can leave a value below 1e-7
+  if (n_term > 0 || ext)
+    for (int i = lane; i < P; i += 64) {
+      if (L.cpu[i] < 1e-7) L.cpu[i] = 0;
+      if (L.mem[i] < 1e-7) L.mem[i] = 0;
+    }
   STAMP(2);
   // ---- _accept_vm_requests (env.py:271-293) ----
+  // only a finish makes a NULL slot: none if the previous per-step launch left
+  // none (EnvHdr::pad bit 32 clear under bit 63; the launch's first step: the
+  // header's hint is the state before it) and none finished now
+  const uint64_t ph = H->pad;
+  const bool no_null = kstep == 0 && (ph >> 63) && !((ph >> 32) & 1u) && n_term == 0;
   int n_null = 0;
+  if (!no_null) {
 #pragma unroll
-  for (int s = 0; s < VPT; s++) {
-    const int v = s * 64 + lane;
-    const bool isnull = w_pl(wa[s]) == NUL;
-    const uint64_t nm = ballot(isnull);
-    if (isnull) L.nulls[n_null + below(nm, lane)] = (uint16_t)v;
-    n_null += __popcll(nm);
+    for (int s = 0; s < VPT; s++) {
+      const int v = s * 64 + lane;
+      const bool isnull = w_pl(wa[s]) == NUL;
+      const uint64_t nm = ballot(isnull);
+      if (isnull) L.nulls[n_null + below(nm, lane)] = (uint16_t)v;
+      n_null += __popcll(nm);
+    }
   }
   const int64_t arrivals = L.arr[kstep];  // rng3.poisson(lambda), drawn in the prologue
   const int64_t k = arrivals < n_null ? arrivals : n_null;
@@ -1610,19 +1622,27 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
   // by k_target_means (vmp_get_stats), so the step skips the two V-long sums.
   const bool kl = p.reward == 2;
   int n_ex = 0, n_w = 0;
+  // wr after a quiet step in which nothing finished, arrived or was placed:
+  // the VM set is the previous step's, so is its waiting ratio (stored in the
+  // header) and whether any VM exists (has_ex: carried by the caller, from
+  // EnvHdr::pad bit 61 at the launch's start)
+  const bool same_vms = p.reward == 0 && quiet_in && n_term == 0 && k == 0;
+  if (!same_vms) {
 #pragma unroll
-  for (int s = 0; s < VPT; s++) {
-    const int c = w_pl(wa[s]);
-    const bool ex = c <= WAIT;
-    const uint64_t em = ballot(ex);
-    if (kl && ex) {
-      const int rk = n_ex + below(em, lane);
-      L.ccomp[rk] = (uint8_t)w_cc(wa[s]);
-      L.mcomp[rk] = (uint8_t)w_cm(wa[s]);
+    for (int s = 0; s < VPT; s++) {
+      const int c = w_pl(wa[s]);
+      const bool ex = c <= WAIT;
+      const uint64_t em = ballot(ex);
+      if (kl && ex) {
+        const int rk = n_ex + below(em, lane);
+        L.ccomp[rk] = (uint8_t)w_cc(wa[s]);
+        L.mcomp[rk] = (uint8_t)w_cm(wa[s]);
+      }
+      n_ex += __popcll(em);
+      n_w += __popcll(ballot(c == WAIT));
     }
-    n_ex += __popcll(em);
-    n_w += __popcll(ballot(c == WAIT));
   }
+  if (!same_vms) has_ex = n_ex > 0;
   wsync();
   STAMP(11);
   // the pairwise reductions of the step, one inlined body per source type:
@@ -1676,14 +1696,14 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
     }
   }
   STAMP(12);
-  const double wr = n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
+  const double wr = same_vms ? H->waiting_ratio : n_ex > 0 ? (double)n_w / (double)n_ex : 0.0;
   if (!kl) res[2] = res[3] = 0.0;  // unused below
   double tcm = res[2] / (double)P;
   if (p.cap_target_util && tcm > 1) tcm = 1.0;
   double tmm = res[3] / (double)P;
   if (p.cap_target_util && tmm > 1) tmm = 1.0;
   double reward = 0.0;
-  if (n_ex > 0) {
+  if (has_ex) {
     if (p.reward == 2) {  // kl (env.py:124-149)
       double cv = res[6] / (double)P, mv = res[7] / (double)P;
       if (cv == 0) cv = 1e-6;
@@ -1705,6 +1725,7 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
   const int64_t ts = H->timestep;
   terminated = ts >= p.limit;
   calm = n_term == 0 && k == 0;  // no PM load fell, no new pending VM
+  (void)n_ex;
   wsync();
   if (lane == 0) {
     H->timestep = ts + 1;
@@ -1904,6 +1925,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   // EnvHdr::pad bit 62 (see heuristic_apply); the external-action kernel
   // neither uses nor keeps it
   bool quiet = !EXT && ((L.hdr->pad >> 62) & 1u);
+  bool has_ex = (L.hdr->pad >> 61) & 1u;  // bit 61: some VM exists (read with bit 62 only)
 #pragma unroll 1
   for (int k = 0; k < k_steps; k++) {
     const bool last = k == k_steps - 1;
@@ -1957,8 +1979,8 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     }
     wsync();
     bool calm = false;
-    const double r = env_tail<VPT, ONE>(p, L, T, wa, rem, run0, fb, dirty, vmo, k, term,
-                                        calm STAMP_ARGS);
+    const double r = env_tail<VPT, ONE>(p, L, T, wa, rem, run0, fb, dirty, vmo, k, EXT, quiet,
+                                        term, calm, has_ex STAMP_ARGS);
     quiet = !EXT && !fit_any && calm;
     if (o.reward && lane == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
@@ -2018,7 +2040,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
         }
         hint = (1ull << 63) | ((uint64_t)nn << 32) | m;
       }
-      hint |= (uint64_t)quiet << 62;
+      hint |= ((uint64_t)quiet << 62) | ((uint64_t)has_ex << 61);
       wsync();
       if (lane == 0) L.hdr->pad = hint;
       wsync();

@@ -43,11 +43,12 @@ struct alignas(16) EnvHdr {
   int64_t total_requests, served, suspend_action, place_action, dropped;
   double total_cpu_req, total_mem_req, waiting_ratio, tcm, tmm;
   // per-step kernels' hint for the next launch's draws (predraw): bit 63
-  // valid, bits 32..61 NULL slots after the step, bits 0..31 the smallest
+  // valid, bits 32..60 NULL slots after the step, bits 0..31 the smallest
   // finish key of the VMs still running (0: no hint). Bit 62 (any k_env
   // launch): "quiet" - no pending VM fit any PM at the last step and no VM
   // finished or arrived in it, so the next heuristic pass places nothing
-  // (written 0 by k_reset, k_env_ext and k_env_big)
+  // (written 0 by k_reset, k_env_ext and k_env_big). Bit 61, read only with
+  // bit 62: some VM existed after the step (the wr reward's n_ex > 0)
   uint64_t pad;
 };
 static_assert(sizeof(EnvHdr) == 256, "EnvHdr must be 256 B");
