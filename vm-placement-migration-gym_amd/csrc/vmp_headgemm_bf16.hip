@@ -67,6 +67,7 @@ constexpr float kLog2e = 1.44269504088896341f;
 
 struct H16Args {
   int B, K, V, A, W32, n_tiles, m_blocks, m_groups, ld;
+  int team, teams;  // XCD teams (launch_hg16); team 0: one column tile per block index
   const uint16_t *h, *w;
   const float *bias;
   const uint32_t *bits;
@@ -156,7 +157,23 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   float LDSP *biasL = reinterpret_cast<float LDSP *>(lds + 2 * kStage);
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int q = lane >> 4, c = lane & 15;
-  const int n_tile = blockIdx.x % a.n_tiles, g = blockIdx.x / a.n_tiles;
+  int n_tile, g;
+  if (a.team > 0) {
+    // XCD teams: blocks b and b + 8 share an XCD (dealt round-robin), so the
+    // team members i = b / 8 .. of one XCD take the same column tile (its W
+    // tile stays in that XCD's L2 while they walk M blocks j, j + G, ...) and
+    // the 32 / team teams resident on an XCD walk the same M blocks (h tiles
+    // shared): at team 8, an L2 working set of 4 W tiles + 8 h tiles instead
+    // of 32 W tiles (VMP_HG16_TEAM: 0 / 2 / 4 / 8 measured, r04_hg16_team.log)
+    const int b = blockIdx.x, i = b >> 3;
+    const int T = (i / a.team) * 8 + (b & 7);
+    if (T >= a.teams) return;  // padding to whole teams on every XCD
+    n_tile = T % a.n_tiles;
+    g = (T / a.n_tiles) * a.team + i % a.team;
+  } else {
+    n_tile = blockIdx.x % a.n_tiles;
+    g = blockIdx.x / a.n_tiles;
+  }
   const int v0 = n_tile * S;
 
   // the tile's bias in tile-column order (0 past A / past V)
@@ -449,7 +466,9 @@ int pick_groups(int n_tiles, int m_blocks) {
 
 template <bool BWD, int NW>
 hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
-  const dim3 grid((unsigned)((int64_t)a.n_tiles * a.m_groups)), block(64 * NW);
+  const int64_t n_wg = a.team > 0 ? (int64_t)(a.teams + 7) / 8 * 8 * a.team
+                                  : (int64_t)a.n_tiles * a.m_groups;
+  const dim3 grid((unsigned)n_wg), block(64 * NW);
   switch (TS) {
 #define VMP_HG16_CASE(T) \
   case T: hipLaunchKernelGGL((k_hg16<T, BWD, NW>), grid, block, lds_bytes<T>(), st, a); break;
@@ -467,7 +486,30 @@ hipError_t launch_hg16(H16Args &a, hipStream_t st) {
   const int S = kMaxNT / TS;
   a.n_tiles = (a.V + S - 1) / S;
   a.m_blocks = (a.B + kBM - 1) / kBM;
-  a.m_groups = pick_groups(a.n_tiles, a.m_blocks);
+  const char *te = getenv("VMP_HG16_TEAM");
+  const int team = te ? atoi(te) : 8;
+  a.team = 0;
+  if (team > 0 && a.m_blocks >= team) {
+    // r walks per team member: the grid n_tiles x team x r (rounded to whole
+    // teams per XCD) whose last round of 256 one-per-CU workgroups is fullest
+    int best = 1;
+    double best_eff = -1.0;
+    for (int r = 1; r * team <= a.m_blocks && r <= 64; r++) {
+      const int64_t teams = (int64_t)a.n_tiles * r;
+      const int64_t wg = (teams + 7) / 8 * 8 * team;
+      const double eff = (double)(teams * team) / ((double)((wg + 255) / 256) * 256.0);
+      if (eff > best_eff + 1e-9) {
+        best_eff = eff;
+        best = r;
+      }
+      if (eff > 0.97) break;
+    }
+    a.team = team;
+    a.teams = a.n_tiles * best;
+    a.m_groups = team * best;
+  } else {
+    a.m_groups = pick_groups(a.n_tiles, a.m_blocks);
+  }
   return launch_ts<BWD, 8>(a, TS, st);
 }
 
