@@ -144,12 +144,155 @@ __device__ __forceinline__ void load_mask(const H16Args &a, int64_t row, uint32_
   mw[W32 - 1] &= tail >= 32 ? ~0u : (1u << tail) - 1u;
 }
 
+// The workgroup's column tile and M group. XCD teams (a.team > 0): blocks b
+// and b + 8 share an XCD (dealt round-robin), so the team members i = b / 8 ..
+// of one XCD take the same column tile (its W tile stays in that XCD's L2
+// while they walk M blocks j, j + G, ...) and the 32 / team teams resident on
+// an XCD walk the same M blocks (h tiles shared): at team 8, an L2 working set
+// of 4 W tiles + 8 h tiles instead of 32 W tiles (VMP_HG16_TEAM: 0 / 2 / 4 / 8
+// measured, profiles/r04_hg16_team.log). False: a padding block.
+__device__ __forceinline__ bool hg16_tile(const H16Args &a, int &n_tile, int &g) {
+  if (a.team > 0) {
+    const int b = blockIdx.x, i = b >> 3;
+    const int T = (i / a.team) * 8 + (b & 7);
+    if (T >= a.teams) return false;  // padding to whole teams on every XCD
+    n_tile = T % a.n_tiles;
+    g = (T / a.n_tiles) * a.team + i % a.team;
+  } else {
+    n_tile = blockIdx.x % a.n_tiles;
+    g = blockIdx.x / a.n_tiles;
+  }
+  return g < a.m_blocks;
+}
+
+// The epilogue of one M block: per sample column mc, per segment s, in registers.
+template <int TS, bool BWD, int NW>
+__device__ __forceinline__ void hg16_epilogue(const H16Args &a,
+                                              f32x4 (&acc)[kMaxNT / TS * TS][16 / NW], int m0,
+                                              int v0, int wid, int lane) {
+  constexpr int S = kMaxNT / TS, MC = 16 / NW;
+  constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
+  const int q = lane >> 4, c = lane & 15;
+  // ---- epilogue: per sample column mc, per segment s, in registers ----
+#pragma unroll
+  for (int mc = 0; mc < MC; mc++) {
+    const int m = m0 + 16 * (MC * wid + mc) + c;
+    const bool live = m < a.B;
+    const int mm = live ? m : a.B - 1;
+    float glp = 0.f, gen = 0.f;
+    if (BWD) {
+      glp = a.g_lp ? a.g_lp[mm] : 0.f;
+      gen = a.g_ent ? a.g_ent[mm] : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+      const int v = v0 + s;
+      if (v >= a.V) break;  // workgroup-uniform: the last tile's missing segments
+      const int64_t row = (int64_t)mm * a.V + v;
+      uint32_t mw[4];
+      load_mask<W32>(a, row, mw);
+      const int act = a.action[row];
+      const int tgt = (act >= 0 && act < a.A) ? act : -1;
+      // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
+      float xm[TS][4];
+      uint32_t nib[TS];
+      float mx = kPad;
+#pragma unroll
+      for (int u = 0; u < TS; u++) {
+        nib[u] = mw[u >> 1] >> (16 * (u & 1) + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = 16 * u + 4 * q + r;
+          const float x = ((nib[u] >> r) & 1u) ? kMasked : acc[s * TS + u][mc][r];
+          // TS = ceil(A / 16): only the segment's last tile reaches past A
+          xm[u][r] = (u < TS - 1 || j < a.A) ? x : kPad;
+          mx = fmaxf(mx, xm[u][r]);
+        }
+      }
+      mx = xmax(mx);
+      // pass 2: p = exp(x - m) (x - m first: exact at x = m, so an all-masked
+      // row gets p = 1 everywhere, as the unfused head), S, T = sum p x
+      float p[TS][4];
+      float Ss = 0.f, Ts = 0.f;
+#pragma unroll
+      for (int u = 0; u < TS; u++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          p[u][r] = __builtin_amdgcn_exp2f((xm[u][r] - mx) * kLog2e);
+          Ss += p[u][r];
+          Ts = __builtin_fmaf(p[u][r], xm[u][r], Ts);
+        }
+      float xa = 0.f;
+      if (!BWD) {  // the given action's logit: tile u_t, register r_t of lane q_t
+        const int ut = tgt >> 4, rt = tgt & 3, qt = (tgt >> 2) & 3;
+        float sel[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < TS; u++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) sel[r] = u == ut ? xm[u][r] : sel[r];
+        xa = rt == 0 ? sel[0] : rt == 1 ? sel[1] : rt == 2 ? sel[2] : sel[3];
+        xa = (tgt >= 0 && q == qt) ? xa : 0.f;
+      }
+      Ss = xsum(Ss);
+      Ts = xsum(Ts);
+      const float lse = mx + logf(Ss);
+      const float inv = 1.0f / Ss;
+      const float H = lse - Ts * inv;  // Categorical.entropy, the tiled head's order
+      if (!BWD) {
+        xa = xsum(xa);  // one lane-element holds it, the others 0
+        if (live && q == 0) {
+          a.row_lp[row] = tgt >= 0 ? xa - lse : NAN;
+          a.row_ent[row] = H;
+        }
+      } else {
+        const float c1 = glp + gen * (H - lse);
+        // pass 1's per-element mask compares are recomputed from the nibbles
+        // here (kept live across pass 2 they are 64-bit SGPR pairs each, and
+        // spilled)
+#pragma unroll
+        for (int u = 0; u < TS; u++) asm volatile("" : "+v"(nib[u]));
+        int tq = tgt - 4 * q;
+        asm volatile("" : "+v"(tq));
+#pragma unroll
+        for (int u = 0; u < TS; u++) {
+          float d[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int j = 16 * u + 4 * q + r;
+            float dd = -(p[u][r] * inv) * __builtin_fmaf(gen, xm[u][r], c1);
+            dd += (16 * u + r == tq) ? glp : 0.f;
+            d[r] = (j < a.A && !((nib[u] >> r) & 1u)) ? dd : 0.f;
+          }
+          // bf16 dlogits (round to nearest even), columns v A + j of row m
+          const int j0 = 16 * u + 4 * q;
+          const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
+          const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
+          const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
+          uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
+          if (u < TS - 1 && ((a.A | a.ld) & 1) == 0) {
+            // the segment's inner tiles hold only real columns (TS = ceil(A / 16)):
+            // the lane's one condition is its sample
+            if (live) {
+              *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
+              *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
+            }
+          } else if (live && j0 < a.A) {
+            dst[0] = u0;
+            if (j0 + 1 < a.A) dst[1] = u1;
+            if (j0 + 2 < a.A) dst[2] = u2;
+            if (j0 + 3 < a.A) dst[3] = u3;
+          }
+        }
+      }
+    }
+  }
+}
+
 // NW waves per workgroup, each owning MC = 16 / NW columns of 16 samples
-// (built: 8 waves x 2 columns, two waves per SIMD)
+// (built: 8 waves x 2 columns, two waves per SIMD). Two LDS stages of BK = 64.
 template <int TS, bool BWD, int NW>
 __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
-  constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
   constexpr int MC = 16 / NW, kThreads = 64 * NW;
   constexpr int kStageW = BNp * kRow, kStage = kStageW + kBM * kRow;
   extern __shared__ __align__(16) char lds_raw[];
@@ -158,22 +301,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int q = lane >> 4, c = lane & 15;
   int n_tile, g;
-  if (a.team > 0) {
-    // XCD teams: blocks b and b + 8 share an XCD (dealt round-robin), so the
-    // team members i = b / 8 .. of one XCD take the same column tile (its W
-    // tile stays in that XCD's L2 while they walk M blocks j, j + G, ...) and
-    // the 32 / team teams resident on an XCD walk the same M blocks (h tiles
-    // shared): at team 8, an L2 working set of 4 W tiles + 8 h tiles instead
-    // of 32 W tiles (VMP_HG16_TEAM: 0 / 2 / 4 / 8 measured, r04_hg16_team.log)
-    const int b = blockIdx.x, i = b >> 3;
-    const int T = (i / a.team) * 8 + (b & 7);
-    if (T >= a.teams) return;  // padding to whole teams on every XCD
-    n_tile = T % a.n_tiles;
-    g = (T / a.n_tiles) * a.team + i % a.team;
-  } else {
-    n_tile = blockIdx.x % a.n_tiles;
-    g = blockIdx.x / a.n_tiles;
-  }
+  if (!hg16_tile(a, n_tile, g)) return;
   const int v0 = n_tile * S;
 
   // the tile's bias in tile-column order (0 past A / past V)
@@ -184,17 +312,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   __syncthreads();
 
   const int nk = a.K / kBK;
-  // VMP_HG16_PRE: the epilogue's mask words and actions are loaded during the
-  // last K stage (their latency under its MFMAs)
-#ifdef VMP_HG16_PRE  // measured: +1 ms on the V300 forward (register pressure), off
-  constexpr bool kPre = MC * S * (W32 + 1) <= (BWD ? 12 : 20);
-#else
-  constexpr bool kPre = false;
-#endif
-  constexpr int kPS = kPre ? S : 1;
-  uint32_t pmw[MC][kPS][4];
-  int pact[MC][kPS];
-
   int sb = 0;  // LDS stage of K step 0 of this M block
   // K step 0 of the first M block; later blocks' step 0 is issued during the
   // previous block's last K step, into the stage that step does not read
@@ -217,26 +334,11 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
     for (int s = 0; s < nk; s++) {
       const char LDSP *cur = lds + ((sb + s) & 1) * kStage;
       char LDSP *nxt = lds + ((sb + s + 1) & 1) * kStage;
-      if (s + 1 < nk) {
+      if (s + 1 < nk)
         stage_issue<TS, NT, NW>(a, nxt, v0, m0, (s + 1) * kBK, wid, lane);
-      } else {
-        if (mn < a.m_blocks) stage_issue<TS, NT, NW>(a, nxt, v0, mn * kBM, 0, wid, lane);
-        if (kPre) {
-#pragma unroll
-          for (int mc = 0; mc < MC; mc++) {
-            const int m = m0 + 16 * (MC * wid + mc) + c;
-            const int64_t rb = (int64_t)(m < a.B ? m : a.B - 1) * a.V;
-#pragma unroll
-            for (int s2 = 0; s2 < kPS; s2++) {
-              const int64_t row = rb + min(v0 + s2, a.V - 1);
-              load_mask<W32>(a, row, pmw[mc][s2]);
-              pact[mc][s2] = a.action[row];
-            }
-          }
-        }
-      }
+      else if (mn < a.m_blocks)
+        stage_issue<TS, NT, NW>(a, nxt, v0, mn * kBM, 0, wid, lane);
       const char LDSP *Hs = cur + kStageW;
-#if !defined(VMP_HG16_NOPIPE)
       // the stage's 2 x NT W fragments are read kPipe ahead of their two MFMAs
       // (an LDS read's latency is several 16-cycle MFMA pairs: read right
       // before its use, every pair waited on it); both K halves' h fragments
@@ -252,6 +354,9 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
 #pragma unroll
       for (int i = 0; i < kPipe; i++) wf[i] = frag(cur, 16 * (i % NT) + c, 4 * (i / NT) + q);
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * MC + kPipe, 0);
+#ifdef VMP_HG16_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int i = 0; i < NF; i++) {
         const int kk = i / NT, nt = i % NT;
@@ -265,50 +370,13 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
       }
-#else
-#pragma unroll
-      for (int kk = 0; kk < 2; kk++) {
-        const int cl = 4 * kk + q;
-        bf16x8 hf[MC];
-#pragma unroll
-        for (int mc = 0; mc < MC; mc++) hf[mc] = frag(Hs, 16 * (MC * wid + mc) + c, cl);
-#if defined(VMP_HG16_HOIST)
-        // the W fragments of VMP_HG16_HOIST tiles are read ahead of their MFMAs,
-        // pinned by a scheduling barrier (left alone, the compiler reads one
-        // fragment, waits for it, and issues its two MFMAs: every LDS latency
-        // exposed)
-        constexpr int G = VMP_HG16_HOIST;
-#pragma unroll
-        for (int n0 = 0; n0 < NT; n0 += G) {
-          bf16x8 wf[G];
-#pragma unroll
-          for (int i = 0; i < G; i++)
-            if (n0 + i < NT) wf[i] = frag(cur, 16 * (n0 + i) + c, cl);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int i = 0; i < G; i++)
-            if (n0 + i < NT)
-#pragma unroll
-              for (int mc = 0; mc < MC; mc++)
-                acc[n0 + i][mc] =
-                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], hf[mc], acc[n0 + i][mc], 0, 0, 0);
-        }
-#else
-#pragma unroll
-        for (int nt = 0; nt < NT; nt++) {
-          const bf16x8 wf = frag(cur, 16 * nt + c, cl);
-#pragma unroll
-          for (int mc = 0; mc < MC; mc++)
-            acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, hf[mc], acc[nt][mc], 0, 0, 0);
-        }
-#endif
-      }
+#ifdef VMP_HG16_PRIO
+      __builtin_amdgcn_s_setprio(0);
 #endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
     sb = (sb + nk) & 1;
-
 #ifdef VMP_HG16_GEMM_ONLY  // timing-only build: the main loop alone (outputs wrong)
 #pragma unroll
     for (int nt = 0; nt < NT; nt++)
@@ -316,124 +384,143 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
       for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
     continue;
 #endif
-    // ---- epilogue: per sample column mc, per segment s, in registers ----
+    hg16_epilogue<TS, BWD, NW>(a, acc, m0, v0, wid, lane);
+  }
+}
+
+// ---- the deep-pipeline kernel: BK = 32 (64-B rows), NS LDS stages ----
+// One stage is (BNp + BM) rows x 64 B (30 KB at NT = 14), so NS - 1 stages are
+// in flight while one is consumed (the two-stage kernel above has one: its
+// 61 KB stages fill LDS at two). The K steps of all the workgroup's M blocks
+// form one sequence, so the next block's first stages load under this block's
+// last MFMAs and its epilogue.
+constexpr int kBK2 = 32;
+constexpr int kRow2 = 2 * kBK2;  // bytes per staged row
+// 16-B chunk c of row r sits at chunk c ^ ((r >> 1) & 3): the 16-lane groups
+// of ds_read_b128 (rows 16 x + c, chunk q) hit 16 distinct bank quads
+__device__ __forceinline__ int lds_chunk2(int row, int cl) { return cl ^ ((row >> 1) & 3); }
+__device__ __forceinline__ bf16x8 frag2(const char LDSP *base, int row, int cl) {
+  return *reinterpret_cast<const bf16x8 LDSP *>(base + row * kRow2 + (lds_chunk2(row, cl) << 4));
+}
+template <int TS, int NT, int NW>
+__device__ __forceinline__ void stage_issue2(const H16Args &a, char LDSP *buf, int v0, int m0,
+                                             int k0, int wid, int lane) {
+  constexpr int SA = 16 * TS, BNp = 16 * NT, PW = BNp / 16, PIECES = (BNp + kBM) / 16;
+  const int rl = lane >> 2, p = lane & 3;
 #pragma unroll
-    for (int mc = 0; mc < MC; mc++) {
-      const int m = m0 + 16 * (MC * wid + mc) + c;
-      const bool live = m < a.B;
-      const int mm = live ? m : a.B - 1;
-      float glp = 0.f, gen = 0.f;
-      if (BWD) {
-        glp = a.g_lp ? a.g_lp[mm] : 0.f;
-        gen = a.g_ent ? a.g_ent[mm] : 0.f;
-      }
-#pragma unroll
-      for (int s = 0; s < S; s++) {
+  for (int i0 = 0; i0 < PIECES; i0 += NW) {
+    const int i = i0 + wid;
+    if (i < PIECES) {  // wave-uniform
+      const uint16_t *src;
+      int r;
+      if (i < PW) {
+        r = 16 * i + rl;
+        const int s = r / SA, j = r - s * SA;
         const int v = v0 + s;
-        if (v >= a.V) break;  // workgroup-uniform: the last tile's missing segments
-        const int64_t row = (int64_t)mm * a.V + v;
-        uint32_t mw[4];
-        int act;
-        if (kPre) {
+        const int wr = (v < a.V && j < a.A) ? v * a.A + j : v0 * a.A;  // pad rows: any row
+        src = a.w + (int64_t)wr * a.K;
+      } else {
+        r = 16 * (i - PW) + rl;
+        src = a.h + (int64_t)min(m0 + r, a.B - 1) * a.K;
+      }
+      src += k0 + 8 * lds_chunk2(r, p);
+      char LDSP *dst = buf + (i < PW ? 0 : BNp * kRow2) + (r - rl) * kRow2;
+      __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)dst, 16, 0, 0);
+    }
+  }
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int TS, bool BWD, int NW, int NS>
+__global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16d(H16Args a) {
+  constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
+  constexpr int MC = 16 / NW, kThreads = 64 * NW;
+  constexpr int kStageW = BNp * kRow2, kStage = kStageW + kBM * kRow2;
+  constexpr int PIECES = (BNp + kBM) / 16, PF = PIECES / NW, PR = PIECES % NW;
+  extern __shared__ __align__(16) char lds_raw[];
+  char LDSP *lds = (char LDSP *)lds_raw;
+  float LDSP *biasL = reinterpret_cast<float LDSP *>(lds + NS * kStage);
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  int n_tile, g;
+  if (!hg16_tile(a, n_tile, g)) return;
+  const int v0 = n_tile * S;
+  for (int n = t; n < BNp; n += kThreads) {
+    const int s = n / SA, j = n - s * SA, v = v0 + s;
+    biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
+  }
+  const int nk = a.K / kBK2;
+  const int nblk = (a.m_blocks - g + a.m_groups - 1) / a.m_groups;
+  const int total = nblk * nk;
+  // stage st: K step st % nk of the workgroup's M block st / nk
+  auto issue = [&](int st) {
+    const int bi = st / nk;
+    stage_issue2<TS, NT, NW>(a, lds + (st % NS) * kStage, v0, (g + bi * a.m_groups) * kBM,
+                             (st - bi * nk) * kBK2, wid, lane);
+  };
 #pragma unroll
-          for (int i = 0; i < 4; i++) mw[i] = pmw[mc][s < kPS ? s : 0][i];
-          act = pact[mc][s < kPS ? s : 0];
-        } else {
-          load_mask<W32>(a, row, mw);
-          act = a.action[row];
-        }
-        const int tgt = (act >= 0 && act < a.A) ? act : -1;
-        // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
-        float xm[TS][4];
-        uint32_t nib[TS];
-        float mx = kPad;
+  for (int st = 0; st < NS - 1; st++)
+    if (st < total) issue(st);
+  f32x4 acc[NT][MC];
+  __syncthreads();  // biasL
 #pragma unroll
-        for (int u = 0; u < TS; u++) {
-          nib[u] = mw[u >> 1] >> (16 * (u & 1) + 4 * q);
+  for (int nt = 0; nt < NT; nt++) {
+    const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
 #pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int j = 16 * u + 4 * q + r;
-            const float x = ((nib[u] >> r) & 1u) ? kMasked : acc[s * TS + u][mc][r];
-            // TS = ceil(A / 16): only the segment's last tile reaches past A
-            xm[u][r] = (u < TS - 1 || j < a.A) ? x : kPad;
-            mx = fmaxf(mx, xm[u][r]);
-          }
-        }
-        mx = xmax(mx);
-        // pass 2: p = exp(x - m) (x - m first: exact at x = m, so an all-masked
-        // row gets p = 1 everywhere, as the unfused head), S, T = sum p x
-        float p[TS][4];
-        float Ss = 0.f, Ts = 0.f;
+    for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
+  }
+#pragma unroll 1
+  for (int st = 0; st < total; st++) {
+    // stage st landed (this wave's pieces; up to NS - 2 later stages stay in
+    // flight: PF or PF + 1 pieces each), then visible to every wave
+    if (st + NS - 2 < total) {
+      if (wid < PR) wait_vmcnt<(NS - 2) * (PF + 1)>();
+      else wait_vmcnt<(NS - 2) * PF>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __syncthreads();
+    // the stage consumed in step st - 1 is free for step st + NS - 1
+    if (st + NS - 1 < total) issue(st + NS - 1);
+    const char LDSP *cur = lds + (st % NS) * kStage;
+    const char LDSP *Hs = cur + kStageW;
+    constexpr int kPipe = VMP_HG16_PIPE;
+    bf16x8 hf[MC];
 #pragma unroll
-        for (int u = 0; u < TS; u++)
+    for (int mc = 0; mc < MC; mc++) hf[mc] = frag2(Hs, 16 * (MC * wid + mc) + c, q);
+    bf16x8 wf[kPipe];
 #pragma unroll
-          for (int r = 0; r < 4; r++) {
-            p[u][r] = __builtin_amdgcn_exp2f((xm[u][r] - mx) * kLog2e);
-            Ss += p[u][r];
-            Ts = __builtin_fmaf(p[u][r], xm[u][r], Ts);
-          }
-        float xa = 0.f;
-        if (!BWD) {  // the given action's logit: tile u_t, register r_t of lane q_t
-          const int ut = tgt >> 4, rt = tgt & 3, qt = (tgt >> 2) & 3;
-          float sel[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < kPipe; i++) wf[i] = frag2(cur, 16 * i + c, q);
+    __builtin_amdgcn_sched_group_barrier(0x100, MC + kPipe, 0);
 #pragma unroll
-          for (int u = 0; u < TS; u++)
+    for (int nt = 0; nt < NT; nt++) {
 #pragma unroll
-            for (int r = 0; r < 4; r++) sel[r] = u == ut ? xm[u][r] : sel[r];
-          xa = rt == 0 ? sel[0] : rt == 1 ? sel[1] : rt == 2 ? sel[2] : sel[3];
-          xa = (tgt >= 0 && q == qt) ? xa : 0.f;
-        }
-        Ss = xsum(Ss);
-        Ts = xsum(Ts);
-        const float lse = mx + logf(Ss);
-        const float inv = 1.0f / Ss;
-        const float H = lse - Ts * inv;  // Categorical.entropy, the tiled head's order
-        if (!BWD) {
-          xa = xsum(xa);  // one lane-element holds it, the others 0
-          if (live && q == 0) {
-            a.row_lp[row] = tgt >= 0 ? xa - lse : NAN;
-            a.row_ent[row] = H;
-          }
-        } else {
-          const float c1 = glp + gen * (H - lse);
-          // pass 1's per-element mask compares are recomputed from the nibbles
-          // here (kept live across pass 2 they are 64-bit SGPR pairs each, and
-          // spilled)
+      for (int mc = 0; mc < MC; mc++)
+        acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt % kPipe], hf[mc], acc[nt][mc], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, MC, 0);
+      if (nt + kPipe < NT) {
+        wf[nt % kPipe] = frag2(cur, 16 * (nt + kPipe) + c, q);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    }
+    const int bi = st / nk;
+    if (st - bi * nk == nk - 1) {  // the M block's last K step: its epilogue
+#ifdef VMP_HG16_GEMM_ONLY
 #pragma unroll
-          for (int u = 0; u < TS; u++) asm volatile("" : "+v"(nib[u]));
-          int tq = tgt - 4 * q;
-          asm volatile("" : "+v"(tq));
+      for (int nt = 0; nt < NT; nt++)
 #pragma unroll
-          for (int u = 0; u < TS; u++) {
-            float d[4];
+        for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
+#else
+      hg16_epilogue<TS, BWD, NW>(a, acc, (g + bi * a.m_groups) * kBM, v0, wid, lane);
+#endif
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-              const int j = 16 * u + 4 * q + r;
-              float dd = -(p[u][r] * inv) * __builtin_fmaf(gen, xm[u][r], c1);
-              dd += (16 * u + r == tq) ? glp : 0.f;
-              d[r] = (j < a.A && !((nib[u] >> r) & 1u)) ? dd : 0.f;
-            }
-            // bf16 dlogits (round to nearest even), columns v A + j of row m
-            const int j0 = 16 * u + 4 * q;
-            const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
-            const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
-            const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
-            uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
-            if (u < TS - 1 && ((a.A | a.ld) & 1) == 0) {
-              // the segment's inner tiles hold only real columns (TS = ceil(A / 16)):
-              // the lane's one condition is its sample
-              if (live) {
-                *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
-                *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
-              }
-            } else if (live && j0 < a.A) {
-              dst[0] = u0;
-              if (j0 + 1 < a.A) dst[1] = u1;
-              if (j0 + 2 < a.A) dst[2] = u2;
-              if (j0 + 3 < a.A) dst[3] = u3;
-            }
-          }
-        }
+      for (int nt = 0; nt < NT; nt++) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
+#pragma unroll
+        for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
       }
     }
   }
@@ -443,6 +530,14 @@ template <int TS>
 constexpr size_t lds_bytes() {
   return 2 * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow + 16 * (kMaxNT / TS * TS) * sizeof(float);
 }
+template <int TS, int NS>
+constexpr size_t lds_bytes_deep() {
+  return NS * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow2 + 16 * (kMaxNT / TS * TS) * sizeof(float);
+}
+#ifndef VMP_HG16_NS
+#define VMP_HG16_NS 4  // deep kernel's LDS stages
+#endif
+static_assert(lds_bytes_deep<1, VMP_HG16_NS>() <= 160 * 1024, "deep stages exceed LDS");
 
 int pick_ts(int A) { return (A + 15) / 16; }  // segment width: 16 TS columns, TS = ceil(A / 16)
 
@@ -469,6 +564,21 @@ hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
   const int64_t n_wg = a.team > 0 ? (int64_t)(a.teams + 7) / 8 * 8 * a.team
                                   : (int64_t)a.n_tiles * a.m_groups;
   const dim3 grid((unsigned)n_wg), block(64 * NW);
+  // VMP_HG16_DEEP=1: the BK = 32 multi-stage kernel (measured slower: forward
+  // 10.3 vs 9.06 ms, backward 14.8 vs 13.3 ms at NS 4 and 5, r04_hg16_deep.log)
+  const char *dp = getenv("VMP_HG16_DEEP");
+  if (dp && dp[0] == '1') {
+    constexpr int NS = VMP_HG16_NS;
+    switch (TS) {
+#define VMP_HG16D_CASE(T) \
+  case T: hipLaunchKernelGGL((k_hg16d<T, BWD, NW, NS>), grid, block, (lds_bytes_deep<T, NS>()), st, a); break;
+      VMP_HG16D_CASE(1) VMP_HG16D_CASE(2) VMP_HG16D_CASE(3) VMP_HG16D_CASE(4)
+      VMP_HG16D_CASE(5) VMP_HG16D_CASE(6) VMP_HG16D_CASE(7)
+      default: hipLaunchKernelGGL((k_hg16d<8, BWD, NW, NS>), grid, block, (lds_bytes_deep<8, NS>()), st, a); break;
+#undef VMP_HG16D_CASE
+    }
+    return hipGetLastError();
+  }
   switch (TS) {
 #define VMP_HG16_CASE(T) \
   case T: hipLaunchKernelGGL((k_hg16<T, BWD, NW>), grid, block, lds_bytes<T>(), st, a); break;
