@@ -495,3 +495,73 @@ def test_unknown_reward_function_asserts_at_first_rewarded_step():
             quiet += 1
     assert quiet >= 1  # arrivals at rate 0.05: the first steps have no VM
     env.close()
+
+
+@pytest.mark.parametrize("reward", ["wr", "ut"])
+@pytest.mark.parametrize("big", [False, True], ids=["wave", "block"])
+def test_step_hints_across_launch_kinds_vs_oracle(big, reward, monkeypatch):
+    """The header's step hints (EnvHdr::pad: NULL slots left, next finish key,
+    the quiet bit and 'some VM exists') are written by one launch and read by
+    the next, which may be another kind of launch. A small env that fills up
+    (V 60, 2 arrivals a step, service ~12 steps: quiet steps where nothing fits,
+    finishes or arrives, between refill bursts) is driven by a fixed mix of
+    per-step FirstFit / BestFit launches, fused 3-step rollouts and external
+    steps that suspend some VMs; rewards, the full state and the counters must
+    be the oracle's after every launch (wr takes the stats skip, ut does not)."""
+    from vmp.batched import BatchedVmEnv
+    if big:
+        monkeypatch.setenv("VMP_BIG_KERNEL", "1")
+    base = dict(pms=8, vms=60, arrival_rate=2.0, service_length=12, training_steps=10000,
+                eval_steps=100000, allow_null_action=True, seed=0, reward_function=reward,
+                sequence="uniform", cap_target_util=True, beta=0.5)
+    N, P = 12, 8
+    seeds = np.arange(N, dtype=np.int64) * 3 + 11
+    b = BatchedVmEnv(_cfg(base), N, seeds=seeds, device=DEV)
+    oes = [O.OracleEnv(dict(base, seed=int(s))) for s in seeds]
+    for e, s in zip(oes, seeds):
+        e.eval(False)
+        e.reset(int(s))
+    rng = np.random.default_rng(5)
+    keys = ("vm_placement", "vm_cpu", "vm_memory", "cpu", "memory", "vm_remaining_runtime")
+    kinds = ["ff", "ff", "roll", "bf", "ff", "ext", "ff", "roll", "ff", "ff"]
+    n_quiet_like = 0
+    for t in range(150):
+        kind = kinds[t % len(kinds)]
+        if kind == "roll":
+            rs = b.rollout("firstfit", 3)[0].cpu().numpy()
+            for k in range(3):
+                for i, e in enumerate(oes):
+                    _, r, _, _ = e.step(e.firstfit())
+                    assert rs[k, i] == r, (t, k, i)
+        elif kind == "ext":
+            pl = b.state()["vm_placement"].cpu().numpy()
+            acts = b.heuristic_act("firstfit").cpu().numpy().astype(np.int64)
+            susp = (pl < P) & (rng.random(pl.shape) < 0.1)
+            acts[susp] = P
+            _, rew, _, _ = b.step(torch.tensor(acts, dtype=torch.int32, device=DEV))
+            rew = rew.cpu().numpy()
+            for i, e in enumerate(oes):
+                _, r, _, _ = e.step(acts[i])
+                assert rew[i] == r, (t, i)
+        else:
+            pol = "firstfit" if kind == "ff" else "bestfit"
+            c0 = b.counters().cpu().numpy()
+            obs, rew, _, _, act = b.heuristic_step(pol, want_actions=True)
+            rew, act, obs = rew.cpu().numpy(), act.cpu().numpy(), obs.cpu().numpy()
+            d = b.counters().cpu().numpy() - c0
+            n_quiet_like += int(((d[:, 1] == 0) & (d[:, 3] == 0)).sum())
+            for i, e in enumerate(oes):
+                a = e.firstfit() if kind == "ff" else e.bestfit()
+                assert np.array_equal(a, act[i]), (t, i)
+                o, r, _, _ = e.step(a)
+                assert rew[i] == r, (t, i, rew[i], r)
+                assert np.array_equal(o, obs[i]), (t, i)
+        sd = {k: v.cpu().numpy() for k, v in b.state().items()}
+        ctr = b.counters().cpu().numpy()
+        for i, e in enumerate(oes):
+            so = e.state()
+            for j, k in enumerate(keys):
+                assert np.array_equal(sd[k][i], so[j]), (t, i, k)
+            assert np.array_equal(ctr[i], e.counters()[0]), (t, i)
+    assert n_quiet_like > 100, "no quiet per-step launches in the mix"
+    b.close()
