@@ -123,6 +123,34 @@ __device__ __forceinline__ float xmax(float v) {
   return fmaxf(v, __shfl_xor(v, 32));
 }
 
+// The row's raw mask words, branch-free (no mask: any readable 16 B, the
+// weight matrix, cleared by mask_fix): loads behind a null test join at a
+// phi, and the compiler waits for them right there instead of at their use.
+template <int W32>
+__device__ __forceinline__ void load_mask_raw(const H16Args &a, int64_t row, uint32_t (&mw)[4]) {
+  const uint32_t *src = a.bits ? a.bits + row * W32 : reinterpret_cast<const uint32_t *>(a.w);
+  mw[0] = mw[1] = mw[2] = mw[3] = 0u;
+  if (W32 == 4) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(src);
+    mw[0] = v[0], mw[1] = v[1], mw[2] = v[2], mw[3] = v[3];
+  } else if (W32 == 2) {
+    const u32x2 v = *reinterpret_cast<const u32x2 *>(src);
+    mw[0] = v[0], mw[1] = v[1];
+  } else {
+#pragma unroll
+    for (int i = 0; i < W32; i++) mw[i] = src[i];
+  }
+}
+// ... at its use: nothing when there is no mask, bits past A cleared
+template <int W32>
+__device__ __forceinline__ void mask_fix(const H16Args &a, uint32_t (&mw)[4]) {
+  const uint32_t on = a.bits ? ~0u : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; i++) mw[i] = i < W32 ? (mw[i] & on) : 0u;
+  const int tail = a.A - 32 * (W32 - 1);  // 1..32 bits in the last word
+  mw[W32 - 1] &= tail >= 32 ? ~0u : (1u << tail) - 1u;
+}
+
 // the row's mask words (bit j of word j >> 5 = action j invalid), bits past A
 // cleared; W32 = ceil(A / 32) words per (sample, VM) row
 template <int W32>
@@ -174,24 +202,46 @@ __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
   constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
   const int q = lane >> 4, c = lane & 15;
   // ---- epilogue: per sample column mc, per segment s, in registers ----
+  // The (mc, s) rows' mask words and actions are loaded one row ahead (and
+  // the backward's per-sample gradients up front), so a row's compute runs
+  // under the next row's loads: loaded where used, every row waited on two
+  // dependent global round trips, and each wait also drained the previous
+  // row's dlogits stores.
+  constexpr int NP = MC * S;
+  auto row_of = [&](int pi) -> int64_t {
+    const int m = m0 + 16 * (MC * wid + pi / S) + c;
+    return (int64_t)(m < a.B ? m : a.B - 1) * a.V + min(v0 + pi % S, a.V - 1);
+  };
+  float glp_[MC], gen_[MC];
 #pragma unroll
   for (int mc = 0; mc < MC; mc++) {
     const int m = m0 + 16 * (MC * wid + mc) + c;
+    const int mm = m < a.B ? m : a.B - 1;
+    glp_[mc] = (BWD && a.g_lp) ? a.g_lp[mm] : 0.f;
+    gen_[mc] = (BWD && a.g_ent) ? a.g_ent[mm] : 0.f;
+  }
+  uint32_t mwn[4];
+  int actn;
+  load_mask_raw<W32>(a, row_of(0), mwn);
+  actn = a.action[row_of(0)];
+#pragma unroll
+  for (int pi = 0; pi < NP; pi++) {
+    const int mc = pi / S, s = pi % S;
+    const int m = m0 + 16 * (MC * wid + mc) + c;
     const bool live = m < a.B;
     const int mm = live ? m : a.B - 1;
-    float glp = 0.f, gen = 0.f;
-    if (BWD) {
-      glp = a.g_lp ? a.g_lp[mm] : 0.f;
-      gen = a.g_ent ? a.g_ent[mm] : 0.f;
+    const float glp = glp_[mc], gen = gen_[mc];
+    uint32_t mw[4] = {mwn[0], mwn[1], mwn[2], mwn[3]};
+    const int act = actn;
+    if (pi + 1 < NP) {
+      load_mask_raw<W32>(a, row_of(pi + 1), mwn);
+      actn = a.action[row_of(pi + 1)];
     }
-#pragma unroll
-    for (int s = 0; s < S; s++) {
+    mask_fix<W32>(a, mw);
+    {
       const int v = v0 + s;
-      if (v >= a.V) break;  // workgroup-uniform: the last tile's missing segments
+      if (v >= a.V) continue;  // workgroup-uniform: the last tile's missing segments
       const int64_t row = (int64_t)mm * a.V + v;
-      uint32_t mw[4];
-      load_mask<W32>(a, row, mw);
-      const int act = a.action[row];
       const int tgt = (act >= 0 && act < a.A) ? act : -1;
       // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
       float xm[TS][4];
