@@ -1823,6 +1823,10 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   // whose latency the random draws below overlap ----
   // (indices are clamped instead of branched on, so no load is conditional and
   // the waits below can count: a skipped load would force vmcnt(0))
+  // a starting wave's state loads issue ahead of the running waves' work: its
+  // critical path starts at their latency (burst launches -1.1-1.6 %,
+  // profiles/r04_prio_prologue_ab.log)
+  __builtin_amdgcn_s_setprio(2);
   const uint64_t hv = gptr(reinterpret_cast<const uint64_t *>(p.hdr + e))[lane & 31];
   // Poisson constants for the block's LDS copy (issued before the state loads,
   // so waiting for them never waits on the state)
@@ -1861,6 +1865,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     }
   }
   __asm__ volatile("" ::: "memory");  // ... and the VM words before any wait
+  __builtin_amdgcn_s_setprio(0);
   // size tables (k/100 in f64 and f32) while the loads are in flight; the only
   // block-wide barrier: waves are independent below
   for (int i = threadIdx.x; i < 128; i += blockDim.x) {
