@@ -404,9 +404,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
 #pragma unroll
       for (int i = 0; i < kPipe; i++) wf[i] = frag(cur, 16 * (i % NT) + c, 4 * (i / NT) + q);
       __builtin_amdgcn_sched_group_barrier(0x100, 2 * MC + kPipe, 0);
-#ifdef VMP_HG16_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int i = 0; i < NF; i++) {
         const int kk = i / NT, nt = i % NT;
@@ -420,9 +417,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
       }
-#ifdef VMP_HG16_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
