@@ -311,7 +311,7 @@ __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
             const int j = 16 * u + 4 * q + r;
             float dd = -(p[u][r] * inv) * __builtin_fmaf(gen, xm[u][r], c1);
             dd += (16 * u + r == tq) ? glp : 0.f;
-            d[r] = (j < a.A && !((nib[u] >> r) & 1u)) ? dd : 0.f;
+            d[r] = ((u < TS - 1 || j < a.A) && !((nib[u] >> r) & 1u)) ? dd : 0.f;  // inner tiles: j < A
           }
           // bf16 dlogits (round to nearest even), columns v A + j of row m
           const int j0 = 16 * u + 4 * q;
