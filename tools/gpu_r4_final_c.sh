@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4 closing check at HEAD: the whole -m gpu suite, smoke(), the driver's
+# default bench line, and the bf16 PPO update after the backward mask change.
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/${1:-r4finalc}; mkdir -p $O
+timeout -k 10 850 python -u -m pytest tests -x -v -m gpu --timeout 400 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?; echo "tests_rc=$rc"; tail -1 $O/gpu_tests.log; [ $rc -ne 0 ] && { grep -E "FAILED|Error" $O/gpu_tests.log | head; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+rc=$?; echo "smoke_rc=$rc"; tail -1 $O/smoke.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2>&1
+rc=$?; echo "bench_rc=$rc"; [ $rc -ne 0 ] && exit $rc
+grep -v amdgpu.ids $O/bench.log | tail -1 | cut -c1-600
+timeout -k 10 300 python tools/bench_ppo.py --precision bf16 --envs 8192 --updates 1 --warmup 1 > $O/ppo_bf16.log 2>&1
+rc=$?; echo "ppo_bf16 rc=$rc"; tail -1 $O/ppo_bf16.log | cut -c1-800; exit $rc
