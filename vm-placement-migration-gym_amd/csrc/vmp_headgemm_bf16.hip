@@ -326,6 +326,13 @@ __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
               *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
               *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
             }
+          } else if (((a.A | a.ld) & 1) == 0) {
+            // the last tile, even A / ld: j0 is a multiple of 4, so the lane's
+            // valid columns are 0, 2 or 4 and come in 4-B aligned pairs
+            if (live && j0 < a.A)
+              *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
+            if (live && j0 + 2 < a.A)
+              *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
           } else if (live && j0 < a.A) {
             dst[0] = u0;
             if (j0 + 1 < a.A) dst[1] = u1;
