@@ -93,6 +93,8 @@ def main():
     ap.add_argument("--no-ppo", action="store_true", help="skip the PPO train / eval legs")
     ap.add_argument("--ppo-envs", type=int, default=8192, help="PPO training envs per GPU")
     ap.add_argument("--ppo-eval-envs", type=int, default=4096)
+    ap.add_argument("--ppo-updates", type=int, default=5,
+                    help="timed collect + update cycles per PPO training leg (median reported)")
     ap.add_argument("--ext-steps", type=int, default=50, help="external-action leg steps")
     ap.add_argument("--stress-ff", type=int, default=2000, help="C5 fast-forward (2*L)")
     ap.add_argument("--stress-steps", type=int, default=20)
@@ -262,12 +264,15 @@ def main():
     bpe = step_bytes(P, V, words, pmw)
     achieved = bpe * N / (kern_ms * 1e-3) / 1e9
     traffic = None
+    issue = None
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             if tj.get("envs") == N and tj.get("bytes_per_launch"):
                 traffic = float(tj["bytes_per_launch"])
+            if tj.get("envs") == N and tj.get("SQ_INSTS_VALU"):
+                issue = issue_roofline(tj, N, kern_ms)
         except Exception:
             traffic = None
     env.close()
@@ -299,7 +304,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "vmp::k_env<16, true> (heuristic act+step, one step per launch)", "kernel_ms": kern_ms,
                      "bytes_per_env_step": bpe, "vm_words_written_per_env_step": words,
-                     "pms_written_per_env_step": pmw},
+                     "pms_written_per_env_step": pmw, "issue": issue},
         "cpu_baseline": cpu,
         "reference_cpu": _reference_cpu(),
         "fused_rollout": {"value": fused_value, "unit": "env-steps/s", "k_steps": kr},
@@ -318,6 +323,35 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+N_SIMDS = 1024  # MI355X: 256 CUs x 4 SIMD-32
+
+
+def issue_roofline(pmc, N, kern_ms):
+    """The headline kernel's instruction-issue ceiling beside its HBM one
+    (VERDICT r4 item 5): instructions per launch from the committed PMC pass
+    (profiles/traffic.json, the same window's SQ_INSTS_* counters) against the
+    issue capacity of the live launch time at the PMC pass's measured clock.
+    VALU: a wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+    (MI355X_MICROARCH.md §Wave scheduling), so busy = 2 x VALU / (1 024 SIMDs x
+    cycles); `valu_frac_single_wave` prices 4 cycles, the rate one wave alone
+    sustains (the figure an issue-bound wave with no co-resident partner
+    would see). The HBM `frac` and this one together bound the kernel."""
+    clk = float(pmc.get("eff_clock_GHz") or 2.4) * 1e9
+    cyc = clk * kern_ms * 1e-3
+    cyc_prof = clk * float(pmc["avg_ns"]) * 1e-9
+    valu, salu = float(pmc["SQ_INSTS_VALU"]), float(pmc.get("SQ_INSTS_SALU", 0.0))
+    lds = float(pmc.get("SQ_INSTS_LDS", 0.0))
+    return {"bound": "valu-issue", "unit": "SIMD issue cycles",
+            "valu_insts_per_env_step": valu / N, "salu_insts_per_env_step": salu / N,
+            "lds_insts_per_env_step": lds / N,
+            "frac": 2.0 * valu / (N_SIMDS * cyc),
+            "frac_at_profile_time": 2.0 * valu / (N_SIMDS * cyc_prof),
+            "valu_frac_single_wave": 4.0 * valu / (N_SIMDS * cyc),
+            "clock_GHz": clk / 1e9, "profile_kernel_ms": float(pmc["avg_ns"]) * 1e-6,
+            "source": "profiles/traffic.json (rocprofv3 --pmc SQ_INSTS_VALU/SALU/LDS, "
+                      "GRBM_GUI_ACTIVE of the headline window)"}
 
 
 def fast_forward(env, policy, seeds, ff, groups, delta, k):
@@ -522,16 +556,20 @@ def cpu_baseline(cfg, threads=0, what="", envs_per_thread=16):
         threads = host["affinity"]
         if host["cgroup_quota_cores"]:
             threads = max(1, min(threads, int(host["cgroup_quota_cores"])))
-    n_env, warm, steps, reps = envs_per_thread * threads, 2500, 1000, 3
+    n_env, warm, steps, reps = envs_per_thread * threads, 2500, 1000, 5
+    # one more pass than reported: the first pass after the warm-up steps is
+    # untimed warm-up of its own (it ran up to 7 % slow on a shared host)
     secs, _ = O.rollout_timed(cfg, n_env, 0, 4, warm, steps, 0, threads, eval_mode=False,
-                              reps=reps)
-    rates = n_env * steps / secs
+                              reps=reps + 1)
+    rates = n_env * steps / secs[1:]
     med = float(np.median(rates))
     return {"value": med, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "repeats": [float(x) for x in rates], "spread": float((rates.max() - rates.min()) / med),
+            "warmup_pass": float(n_env * steps / secs[0]),
             **host,
-            "sample": f"{n_env} envs x {steps} FirstFit act+step per pass, {reps} passes (median), "
-                      f"after {warm} warm-up steps, OpenMP {threads} threads (C oracle, {what})"}
+            "sample": f"{n_env} envs x {steps} FirstFit act+step per pass, {reps} passes (median) "
+                      f"after one untimed pass and {warm} warm-up steps, OpenMP {threads} "
+                      f"threads (C oracle, {what})"}
 
 
 def _guard(fn, *a):
@@ -585,9 +623,10 @@ def mfma_roofline(flops, seconds, precision, what):
 
 def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
     """BASELINE config 3 (config/100.yml, PPO from scratch, reward wr, 8192 envs per
-    GPU): one untimed update, then one timed update = batch_size rollout steps of
-    every env + PPOAgent.update (4 epochs x 4 minibatches), data-parallel over ranks
-    (one RCCL all-reduce of the flat gradient per optimizer step)."""
+    GPU): one untimed collect + update, then --ppo-updates (5) timed cycles of
+    batch_size rollout steps of every env + PPOAgent.update (4 epochs x 4
+    minibatches), data-parallel over ranks (one RCCL all-reduce
+    of the flat gradient per optimizer step). Median and spread reported."""
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
     from vmp.ppo import PPOAgent, PPOConfig
@@ -603,44 +642,59 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
     tr.collect()
     tr.update()
     torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    tr.collect()
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    st = tr.update()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    t2 = time.perf_counter()
-    total = _max_over_ranks(t2 - t0, dev, dist)
-    upd_s = _max_over_ranks(t2 - t1, dev, dist)
-    steps = world * N * tr.T
     H = ag.config.hidden_size
-    fc, fu = ppo_update_flops(env.D, H, env.V * env.A, tr.T, N, st["minibatches"] + st["kl_breaks"],
-                              ag.config.minibatch_size)
     fused = precision == "bf16" and ag.model.bf16_fused()
+    runs = []  # per timed update: (collect s, update s, evaluated minibatches, minibatch steps, kl breaks)
+    for _ in range(max(1, int(args.ppo_updates))):
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        tr.collect()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        st = tr.update()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        t2 = time.perf_counter()
+        runs.append((_max_over_ranks(t1 - t0, dev, dist), _max_over_ranks(t2 - t1, dev, dist),
+                     st["minibatches"] + st["kl_breaks"], st["minibatches"], st["kl_breaks"]))
+    col = np.array([r[0] for r in runs])
+    upd = np.array([r[1] for r in runs])
+    tot = col + upd
+    steps = world * N * tr.T
+    # algorithmic FLOPs of each timed update (the KL early stop may skip minibatches)
+    fus = np.array([ppo_update_flops(env.D, H, env.V * env.A, tr.T, N, r[2],
+                                     ag.config.minibatch_size)[1] for r in runs])
+    fc = ppo_update_flops(env.D, H, env.V * env.A, tr.T, N, 0, ag.config.minibatch_size)[0]
     # the fused head's backward recomputes the last layer's logits: matrix-core
     # work beyond the algorithmic count (what a PMC MFMA-busy pass sees)
-    recompute = ((st["minibatches"] + st["kl_breaks"]) * ag.config.minibatch_size * N
-                 * 2.0 * H * env.V * env.A) if fused else 0.0
+    recompute = np.array([r[2] * ag.config.minibatch_size * N * 2.0 * H * env.V * env.A
+                          for r in runs]) if fused else np.zeros(len(runs))
+    med = int(np.argsort(upd)[len(upd) // 2])  # the median update
+    upd_s, col_s, total = float(upd[med]), float(col[med]), float(np.median(tot))
     env.close()
     return {"value": steps / total, "unit": "env-steps/s",
-            "roofline": dict(mfma_roofline(fu, upd_s, precision,
-                                           "PPOAgent.update (all GEMMs, per GPU) / update wall time"),
-                             executed_flops=fu + recompute),
-            "collect_roofline": mfma_roofline(fc, t1 - t0, precision,
+            "value_kind": f"median over {len(runs)} timed collect + update cycles",
+            "roofline": dict(mfma_roofline(float(fus[med]), upd_s, precision,
+                                           "PPOAgent.update (all GEMMs, per GPU) / update wall "
+                                           "time, median update"),
+                             executed_flops=float(fus[med] + recompute[med])),
+            "collect_roofline": mfma_roofline(fc, col_s, precision,
                                               "rollout actor forward / collect wall time"),
+            "updates_timed": len(runs), "update_s_all": [float(x) for x in upd],
+            "collect_s_all": [float(x) for x in col],
+            "update_s_spread": float((upd.max() - upd.min()) / np.median(upd)),
             "head": ("fused bf16 matrix-core actor head (vmp_actor_head_bf16_fwd/_bwd)" if fused
                      else "f32 logits + HIP head" if precision == "f32"
                      else "bf16 GEMM -> f32 logits + HIP head"),
             "dtype": "f32" if precision == "f32" else "bf16 GEMM inputs, f32 accumulate/params",
             "workload": "config/100.yml (P100 V300), PPO train from scratch, reward wr, "
                         "hidden 512, batch 100 / minibatch 25, 4 epochs",
-            "envs_per_gpu": N, "global_envs": world * N, "updates_timed": 1,
-            "s_per_update": total, "collect_s": t1 - t0, "update_s": t2 - t1,
-            "minibatch_steps": st["minibatches"], "kl_breaks": st["kl_breaks"],
+            "envs_per_gpu": N, "global_envs": world * N,
+            "s_per_update": total, "collect_s": float(np.median(col)),
+            "update_s": float(np.median(upd)), "update_s_min": float(upd.min()),
+            "minibatch_steps": [r[3] for r in runs], "kl_breaks": [r[4] for r in runs],
             "parallelism": f"data-parallel x{world} (RCCL grad all-reduce)" if world > 1
             else "single GPU"}
 

@@ -192,6 +192,21 @@ int vmp_get_state(vmp_handle *h, int64_t *placement, double *vm_cpu, double *vm_
 /* _get_rank (env.py:320-325) = number of PMs hosting >= 1 VM: int64[n_env]. */
 int vmp_get_rank(vmp_handle *h, int64_t *rank);
 
+/* Checkpoint / resume of the batched env state (the reference only
+ * saves the policy weights, ppo.py:163-170). vmp_snapshot copies everything a
+ * later reset/step reads — the four PCG64 streams and sequence bases, counters,
+ * step hints, PM resources and VM words with their finish keys — into a
+ * device buffer of vmp_snapshot_bytes() bytes (16-byte aligned); vmp_restore
+ * writes it into a handle of the same env count and config (the config's seed
+ * field may differ), which then continues bit-exactly where the snapshotted
+ * handle stood. Stream-ordered on the handle's stream (vmp_snapshot returns
+ * after the copy; vmp_restore synchronises the stream once to check the
+ * snapshot's descriptor). Not included: eval mode (vmp_set_eval) and the
+ * Record recorder (re-enable it after a restore, as after a reset). */
+int vmp_snapshot_bytes(const vmp_handle *h, int64_t *bytes);
+int vmp_snapshot(vmp_handle *h, void *dst);
+int vmp_restore(vmp_handle *h, const void *src);
+
 /* PPOAgent.update GAE (ppo.py:232-243) over T steps x N envs, reverse scan:
  *  delta = r + (1-d)*gamma*v' - v;  g = delta + (1-d)*gamma*lambda*g.
  * All device f32 [T][N] (done as f32 0/1); adv and ret are outputs. */
@@ -265,7 +280,8 @@ int vmp_actor_head(int32_t B, int32_t K, int32_t V, int32_t A, int32_t mode, con
  * trains in f32). h bf16[B][K] (the actor's last hidden layer rounded to
  * bf16), weight bf16[V*A][K], bias f32[V*A], mask_bits as vmp_policy_head
  * (nullable), action i32[B][V] (GIVEN). Needs K % 64 == 0, A <= 128, 16-byte
- * aligned h / weight.
+ * aligned h / weight / mask_bits (a row's mask words are read as one vector)
+ * and, for the backward, 4-byte aligned dlogits (stored as bf16 pairs).
  * Forward: logprob / entropy f32[B] of the given actions; logits formed tile
  * by tile on the bf16 matrix cores (f32 accumulate) and consumed in
  * registers, never written. workspace: nullable, 2*B*V floats. */
@@ -311,6 +327,14 @@ int64_t vmp_debug_live_allocs(void);
  * Only a library built with -DVMP_STAMPS records them; otherwise
  * returns VMP_EINVAL. */
 int vmp_debug_stamps(vmp_handle *h, uint64_t *out);
+
+/* Diagnostics (-DVMP_CHECK_QUIET check build, `make check-quiet`): the number
+ * of per-step launches, since the previous call, that skipped the heuristic
+ * on the header's quiet bit (EnvHdr::pad bit 62) although some pending VM
+ * fitted a PM — always 0 unless an entry point that writes env state left the
+ * bit stale. The check build evaluates the fit test on quiet steps too.
+ * Returns VMP_EINVAL in a normal build. */
+int vmp_debug_quiet_violations(int64_t *count);
 
 /* Diagnostics: workgroups per CU the runtime reports for the per-step env
  * kernel of this handle (hipOccupancyMaxActiveBlocksPerMultiprocessor) and

@@ -5,7 +5,10 @@ the same bf16 leg (BF16ActorHead: hipBLASLt bf16 GEMM with f32 logits + the
 tiled HIP head) and a plain-PyTorch fp32 head on the same bf16-rounded
 operands. Tolerances: logprob / entropy 1e-5 relative (f32 accumulation of
 the same bf16 products in another order); parameter gradients 1e-3 relative
-L2 (both paths round dlogits to bf16 before the dW / dh GEMMs). Memory: a
+L2 against the logits path (both paths round dlogits to bf16 before the
+dW / dh GEMMs) and 1e-2 relative L2 against torch fp32 autograd of a
+plain-PyTorch head on the bf16-rounded operands (no HIP code on that side:
+the fused path's only extra rounding is its bf16 dlogits). Memory: a
 bf16 update on the fused path stays below one minibatch's f32 [B, V*A]
 logits; the logits path does not."""
 import numpy as np
@@ -45,6 +48,21 @@ def _case(B, K, V, A, seed, p_mask=0.4):
 
 def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp(min=1e-30))
+
+
+def _torch_fp32_grads(h, w, b, bits, act, V, A, glp, gen):
+    """d/d(h, W, b) of sum(glp * logprob + gen * entropy) by torch autograd in
+    fp32: logits = b + bf16(h) bf16(W)^T as fp32 addmm, the masked head in plain
+    PyTorch (tests/torch_ref.torch_head: masked_fill, logsumexp, softmax). The
+    out-of-row action of row 0 is clamped into the row; callers give row 0 a
+    zero logprob weight."""
+    hr = h.bfloat16().float().requires_grad_(True)
+    wr = w.bfloat16().float().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    logits = torch.addmm(br, hr, wr.t())
+    _, lp, ent = torch_head(logits, V, A, bits=bits, action=act.long().clamp(0, A - 1))
+    ((lp * glp).sum() + (ent * gen).sum()).backward()
+    return hr.grad, wr.grad, br.grad
 
 
 def _run(fused, h, w, b, bits, act, V, A, glp, gen, chunk_rows=1 << 20):
@@ -90,6 +108,12 @@ def test_fused_matches_logits_path_and_torch(B, K, V, A):
     for name, f, u in (("x", gx_f, gx_u), ("w", gw_f, gw_u), ("b", gb_f, gb_u)):
         assert torch.isfinite(f).all(), name
         assert _rel(f, u) < 1e-3, (name, _rel(f, u))
+    # independent of every HIP path: torch fp32 autograd through a plain-PyTorch
+    # head on the bf16-rounded operands (the fused path rounds dlogits to bf16
+    # before its dW / dh GEMMs: 1e-2 relative L2 allowed, ~2e-3 expected)
+    gx_r, gw_r, gb_r = _torch_fp32_grads(h, w, b, bits, act, V, A, glp0, gen)
+    for name, f, r in (("x", gx_f, gx_r), ("w", gw_f, gw_r), ("b", gb_f, gb_r)):
+        assert _rel(f, r) < 1e-2, (name, "vs fp32 autograd", _rel(f, r))
     # chunking does not change the result: one chunk == many chunks (same sums per chunk row)
     _, _, gx_1, gw_1, gb_1 = _run(True, h, w, b, bits, act, V, A, glp0, gen, chunk_rows=1 << 20)
     assert _rel(gx_1, gx_f) < 1e-6 and _rel(gw_1, gw_f) < 1e-6 and _rel(gb_1, gb_f) < 1e-6

@@ -131,6 +131,9 @@ def _install_step_trace(agent, trace):
     the parameters after every AdamW step, and per evaluated minibatch the new
     log-probabilities and values the loss used."""
     m = agent.model
+    # the reference's step sequence exactly: no look-ahead step that a KL break
+    # would roll back (it would show in the trace, not in the parameters)
+    agent.config.kl_lookahead = False
     keys = sorted(m.state_dict())
 
     def flat():
@@ -225,6 +228,35 @@ def test_update_matches_reference_update_100yml(k_epochs):
     ppo100_check(d, ag.model, st, k_epochs)
 
 
+@pytest.mark.parametrize("kl_max", [0.02, 0.004, 0.0005])
+def test_kl_lookahead_equals_synchronous_update(kl_max):
+    """PPOConfig.kl_lookahead (the default): each minibatch's AdamW step is taken
+    before its KL early-stop flag reaches the host and rolled back on a break
+    (ppo.py:263-264). On the reference's 100.yml batch (4 epochs: the golden
+    KL break of epoch 4, and more breaks at tighter kl_max) the accepted steps,
+    the stats and the final parameters and AdamW state must equal the
+    synchronous loop's bit for bit."""
+    out = []
+    for look in (False, True):
+        cfg = dict(CFG10, pms=100, vms=300, arrival_rate=1.8182, service_length=1000, seed=0)
+        ag = PPOAgent(StubEnv(Config(**cfg)), PPOConfig(hidden_size=8, episodes=1, k_epochs=4,
+                                                         kl_max=kl_max, kl_lookahead=look),
+                      head=torch_head, gae=torch_gae)
+        d, ag, st = _ppo100_update(4, agent=ag)
+        out.append((ag, st))
+    (a0, s0), (a1, s1) = out
+    assert s0["kl_breaks"] >= 1, "no KL break: the rollback path is not exercised"
+    for k in ("minibatches", "kl_breaks", "clipfracs", "kl"):
+        assert s0[k] == s1[k], k
+    assert s1["rollbacks"] >= s1["kl_breaks"]
+    for k, v in a0.model.state_dict().items():
+        assert torch.equal(v, a1.model.state_dict()[k]), k
+    o0, o1 = a0.optimizer.state_dict()["state"], a1.optimizer.state_dict()["state"]
+    for i in o0:
+        for k in o0[i]:
+            assert torch.equal(o0[i][k], o1[i][k]), (i, k)
+
+
 def test_elementwise_value_loss_differs():
     """value_loss_broadcast=False is a real change of the loss (not the reference)."""
     d = _golden("ppo_update.npz")
@@ -271,7 +303,7 @@ def test_chunked_update_equals_unchunked():
     roll = _synthetic_rollout(T=20, N=6)
     sd = None
     out = []
-    for cb in (1 << 40, 5 * 30 * 12 * 4 * 2):  # one chunk / 2-env chunks
+    for cb in (1 << 40, 5 * 30 * 12 * 4 * 2):  # one chunk / 1-2-env chunks
         ag = _agent(n_envs=6, batch_size=20, minibatch_size=5, chunk_bytes=cb)
         if sd is None:
             sd = {k: v.clone() for k, v in ag.model.state_dict().items()}

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--hidden", type=int, default=512)
     ap.add_argument("--chunk-gb", type=float, default=0.0, help="0: auto (1/8 of HBM)")
     ap.add_argument("--precision", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--lookahead", type=int, default=1, help="PPOConfig.kl_lookahead")
     args = ap.parse_args()
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
@@ -42,7 +43,7 @@ def main():
     ag = PPOAgent(env, PPOConfig(hidden_size=args.hidden, masked=True, batch_size=100,
                                  minibatch_size=25, migration_ratio=0.002,
                                  chunk_bytes=int(args.chunk_gb * (1 << 30)),
-                                 precision=args.precision))
+                                 precision=args.precision, kl_lookahead=bool(args.lookahead)))
     tr = ag.trainer()
     for _ in range(args.warmup):
         tr.collect()
@@ -61,6 +62,7 @@ def main():
         tu += t2 - t1
     steps = args.envs * tr.T * args.updates
     out = {"workload": f"PPO train P{args.pms} V{args.vms} hidden {args.hidden} {args.precision}",
+           "kl_lookahead": bool(args.lookahead),
            "envs": args.envs, "updates": args.updates, "env_steps": steps,
            "value": steps / (tc + tu), "unit": "env-steps/s",
            "collect_s_per_update": tc / args.updates, "update_s_per_update": tu / args.updates,

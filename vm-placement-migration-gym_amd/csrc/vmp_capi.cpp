@@ -42,6 +42,7 @@ __global__ void k_record_init(EnvParams p, RecArgs r);
 __global__ void k_record_close(EnvParams p, RecArgs r, uint32_t *hist, double *sums);
 __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, uint8_t *mask);
 __global__ void k_act_obs(int P, int V, int policy, const float *obs, int32_t *act);
+int64_t quiet_violations_take();
 }  // namespace vmp
 
 using namespace vmp;
@@ -828,7 +829,92 @@ int vmp_get_rank(vmp_handle *h, int64_t *rank) {
   return VMP_OK;
 }
 
+// ---- checkpoint / resume of the batched env state ----
+// Snapshot = a 256-B descriptor, then hdr[N] | pm[N][2P] | vmw[N][V] as the
+// kernels keep them (PCG64 states, sequence bases, counters, step hints and
+// finish keys included), so a restore is bit-exact by construction: the
+// restored handle holds the very bytes every later kernel reads.
+namespace {
+constexpr uint64_t kSnapMagic = 0x31504e534d504d56ULL;  // "VMPMSNP1"
+constexpr int64_t kSnapHead = 256;
+struct SnapDesc {
+  uint64_t magic;
+  int32_t abi, hdr_bytes;
+  int32_t N, P, V, A;
+  vmp_config cfg;  // seed excluded from the compatibility check
+};
+static_assert(sizeof(SnapDesc) <= kSnapHead, "snapshot descriptor exceeds its header");
+int64_t snap_bytes(const vmp_handle *h) {
+  return kSnapHead + (int64_t)sizeof(EnvHdr) * h->N + 16 * (int64_t)h->N * h->P +
+         8 * (int64_t)h->N * h->V;
+}
+bool same_config(const vmp_config &a, const vmp_config &b) {
+  vmp_config x = a, y = b;
+  x.seed = y.seed = 0;
+  return std::memcmp(&x, &y, sizeof(x)) == 0;
+}
+}  // namespace
+
+int vmp_snapshot_bytes(const vmp_handle *h, int64_t *bytes) {
+  if (!h || !bytes) return fail(VMP_EINVAL, "null argument");
+  *bytes = snap_bytes(h);
+  return VMP_OK;
+}
+
+int vmp_snapshot(vmp_handle *h, void *dst) {
+  if (!h || !dst) return fail(VMP_EINVAL, "null argument");
+  if (((uintptr_t)dst) & 15) return fail(VMP_EINVAL, "vmp_snapshot: dst must be 16-byte aligned");
+  uint8_t head[kSnapHead];
+  std::memset(head, 0, sizeof(head));
+  SnapDesc d;
+  std::memset(&d, 0, sizeof(d));
+  d.magic = kSnapMagic;
+  d.abi = VMP_ABI_VERSION;
+  d.hdr_bytes = (int32_t)sizeof(EnvHdr);
+  d.N = h->N, d.P = h->P, d.V = h->V, d.A = h->A;
+  d.cfg = h->cfg;
+  std::memcpy(head, &d, sizeof(d));
+  uint8_t *o = (uint8_t *)dst;
+  const size_t nh = sizeof(EnvHdr) * (size_t)h->N, np = 16 * (size_t)h->N * h->P;
+  HIP_TRY(hipMemcpyAsync(o, head, kSnapHead, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(o + kSnapHead, h->hdr, nh, hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(o + kSnapHead + nh, h->pm, np, hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(o + kSnapHead + nh + np, h->vmw, 8 * (size_t)h->N * h->V,
+                         hipMemcpyDeviceToDevice, h->stream));
+  // the descriptor's host copy is a stack buffer: the call returns after it is read
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return VMP_OK;
+}
+
+int vmp_restore(vmp_handle *h, const void *src) {
+  if (!h || !src) return fail(VMP_EINVAL, "null argument");
+  if (((uintptr_t)src) & 15) return fail(VMP_EINVAL, "vmp_restore: src must be 16-byte aligned");
+  SnapDesc d;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy(&d, src, sizeof(d), hipMemcpyDeviceToHost));
+  if (d.magic != kSnapMagic || d.abi != VMP_ABI_VERSION || d.hdr_bytes != (int32_t)sizeof(EnvHdr))
+    return fail(VMP_EINVAL, "vmp_restore: not a snapshot of this library version");
+  if (d.N != h->N || d.P != h->P || d.V != h->V || d.A != h->A || !same_config(d.cfg, h->cfg))
+    return fail(VMP_EINVAL, "vmp_restore: snapshot of another env count or config");
+  const uint8_t *s = (const uint8_t *)src;
+  const size_t nh = sizeof(EnvHdr) * (size_t)h->N, np = 16 * (size_t)h->N * h->P;
+  HIP_TRY(hipMemcpyAsync(h->hdr, s + kSnapHead, nh, hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->pm, s + kSnapHead + nh, np, hipMemcpyDeviceToDevice, h->stream));
+  HIP_TRY(hipMemcpyAsync(h->vmw, s + kSnapHead + nh + np, 8 * (size_t)h->N * h->V,
+                         hipMemcpyDeviceToDevice, h->stream));
+  return VMP_OK;
+}
+
 int64_t vmp_debug_live_allocs(void) { return g_live.load(); }
+
+int vmp_debug_quiet_violations(int64_t *count) {
+  if (!count) return fail(VMP_EINVAL, "null argument");
+  const int64_t v = quiet_violations_take();
+  if (v == -1) return fail(VMP_EINVAL, "library built without -DVMP_CHECK_QUIET");
+  if (v < 0) return fail(VMP_EDEVICE, "vmp_debug_quiet_violations: device read failed");
+  *count = v;
+  return VMP_OK;
+}
 
 int vmp_debug_fail_alloc(int32_t n) {
   if (n < 0) return fail(VMP_EINVAL, "n must be >= 0");

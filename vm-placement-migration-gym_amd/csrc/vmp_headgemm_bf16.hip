@@ -675,13 +675,17 @@ hipError_t launch_hg16(H16Args &a, hipStream_t st) {
 }
 
 int check_common(int32_t B, int32_t K, int32_t V, int32_t A, const void *h, const void *w,
-                 const float *bias, const int32_t *action, const char *who) {
+                 const float *bias, const uint32_t *bits, const int32_t *action,
+                 const char *who) {
   if (B < 0 || K < 1 || V < 1 || A < 1 || !h || !w || !bias || !action)
     return policy_fail(VMP_EINVAL, who);
   if (K % kBK != 0 || A > VMP_ACTOR_HEAD_MAX_A)
     return policy_fail(VMP_EINVAL, "bf16 actor head: needs K % 64 == 0 and A <= 128");
   if ((((uintptr_t)h) | ((uintptr_t)w)) & 15)
     return policy_fail(VMP_EINVAL, "bf16 actor head: h and weight must be 16-byte aligned");
+  // the epilogue reads a row's ceil(A / 32) mask words as one u32x4 / u32x2
+  if (((uintptr_t)bits) & 15)
+    return policy_fail(VMP_EINVAL, "bf16 actor head: mask_bits must be 16-byte aligned");
   return VMP_OK;
 }
 
@@ -695,7 +699,7 @@ extern "C" int vmp_actor_head_bf16_fwd(int32_t B, int32_t K, int32_t V, int32_t 
                                        const float *bias, const uint32_t *mask_bits,
                                        const int32_t *action, float *logprob, float *entropy,
                                        float *workspace, void *stream) {
-  int rc = check_common(B, K, V, A, h, weight, bias, action,
+  int rc = check_common(B, K, V, A, h, weight, bias, mask_bits, action,
                         "vmp_actor_head_bf16_fwd: bad shape or null pointer");
   if (rc) return rc;
   if (!logprob || !entropy) return policy_fail(VMP_EINVAL, "vmp_actor_head_bf16_fwd: null output");
@@ -732,11 +736,14 @@ extern "C" int vmp_actor_head_bf16_bwd(int32_t B, int32_t K, int32_t V, int32_t 
                                        const int32_t *action, const float *g_logprob,
                                        const float *g_entropy, uint16_t *dlogits, int32_t ld,
                                        void *stream) {
-  int rc = check_common(B, K, V, A, h, weight, bias, action,
+  int rc = check_common(B, K, V, A, h, weight, bias, mask_bits, action,
                         "vmp_actor_head_bf16_bwd: bad shape or null pointer");
   if (rc) return rc;
   if (!dlogits || ld < V * A)
     return policy_fail(VMP_EINVAL, "vmp_actor_head_bf16_bwd: null dlogits or ld < V*A");
+  // even A and ld: the dlogits go out as 4-byte pairs
+  if (((uintptr_t)dlogits) & 3)
+    return policy_fail(VMP_EINVAL, "vmp_actor_head_bf16_bwd: dlogits must be 4-byte aligned");
   if (B == 0) return VMP_OK;
   H16Args a{};
   a.B = B, a.K = K, a.V = V, a.A = A, a.W32 = (A + 31) / 32, a.ld = ld;

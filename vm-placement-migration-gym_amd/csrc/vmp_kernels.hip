@@ -43,6 +43,23 @@ __device__ __forceinline__ T GLBP *gptr(T *p) {
   return (T GLBP *)p;
 }
 
+#ifdef VMP_CHECK_QUIET
+// quiet-bit check build: quiet steps in which some pending VM fit a PM
+__device__ unsigned long long g_quiet_violations;
+#endif
+// -> the count since the last call (reset to 0); -1 in a build without the check
+int64_t quiet_violations_take() {
+#ifdef VMP_CHECK_QUIET
+  unsigned long long v = 0, z = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_quiet_violations), sizeof(v)) != hipSuccess) return -2;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_quiet_violations), &z, sizeof(z)) != hipSuccess) return -2;
+  return (int64_t)v;
+#else
+  return -1;
+#endif
+}
+
 // Streaming stores (obs / state written once per launch, not re-read by it).
 #ifdef VMP_NT_STORE
 #define ST_NT(ptr, val) __builtin_nontemporal_store((val), gptr(ptr))
@@ -1296,8 +1313,15 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
   // quiet (EnvHdr::pad bit 62): the previous step found no pending VM that
   // fits any PM, and since then no VM finished (no PM load fell) and none
   // arrived (no new pending VM): nothing fits now either, so the heuristic
-  // places nothing and the any-fit table need not be built
+  // places nothing and the any-fit table need not be built. The check build
+  // (-DVMP_CHECK_QUIET) builds it anyway and counts the quiet steps in which
+  // some pending VM fits (vmp_debug_quiet_violations): 0 unless a writer of
+  // the env state left a stale bit 62 (see EnvHdr::pad).
+#ifdef VMP_CHECK_QUIET
+  if (ballot(pend != 0)) {
+#else
   if (!quiet && ballot(pend != 0)) {
+#endif
     for (int i = lane; i < P; i += 64) {
       const float fcv = (float)L.cpu[i], fmv = (float)L.mem[i];
       L.fcpu[i] = fcv;
@@ -1317,6 +1341,11 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
       hit |= (uint32_t)(((pend >> s) & 1u) && M[w_cc(wa[s])] > (uint32_t)w_cm(wa[s])) << s;
     const bool anyfit = ballot(hit != 0) != 0;
     fit_any = anyfit;
+#ifdef VMP_CHECK_QUIET
+    if (quiet && anyfit && lane == 0)
+      __hip_atomic_fetch_add(gptr(&g_quiet_violations), 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+#endif
     STAMP(17);
 #pragma unroll 1
     for (; anyfit;) {

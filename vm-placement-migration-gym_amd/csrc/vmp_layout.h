@@ -49,6 +49,11 @@ struct alignas(16) EnvHdr {
   // finished or arrived in it, so the next heuristic pass places nothing
   // (written 0 by k_reset, k_env_ext and k_env_big). Bit 61, read only with
   // bit 62: some VM existed after the step (the wr reward's n_ex > 0)
+  // INVARIANT: any new code path that changes an env's hdr / vmw / pm words
+  // must either write this word as 0 or keep every bit exact for the state it
+  // leaves (vmp_restore copies it with the state it belongs to). A stale bit
+  // 62 silently skips placements: the -DVMP_CHECK_QUIET build counts such
+  // steps (vmp_debug_quiet_violations, tests/test_gpu_env.py).
   uint64_t pad;
 };
 static_assert(sizeof(EnvHdr) == 256, "EnvHdr must be 256 B");

@@ -19,8 +19,9 @@ EXPORTS = (
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
     "vmp_policy_head", "vmp_policy_head_backward", "vmp_policy_head_backward_bf16",
     "vmp_actor_head", "vmp_actor_head_bf16_fwd", "vmp_actor_head_bf16_bwd", "vmp_record_enable",
-    "vmp_record_read",
+    "vmp_record_read", "vmp_snapshot_bytes", "vmp_snapshot", "vmp_restore",
     "vmp_debug_fail_alloc", "vmp_debug_live_allocs", "vmp_debug_stamps", "vmp_debug_occupancy",
+    "vmp_debug_quiet_violations",
 )
 
 
@@ -98,10 +99,14 @@ def lib():
                                                     i32, P]),
         "vmp_record_enable": (ctypes.c_int, [P, i32]),
         "vmp_record_read": (ctypes.c_int, [P, P, P]),
+        "vmp_snapshot_bytes": (ctypes.c_int, [P, P]),
+        "vmp_snapshot": (ctypes.c_int, [P, P]),
+        "vmp_restore": (ctypes.c_int, [P, P]),
         "vmp_debug_fail_alloc": (ctypes.c_int, [i32]),
         "vmp_debug_live_allocs": (ctypes.c_int64, []),
         "vmp_debug_stamps": (ctypes.c_int, [P, P]),
         "vmp_debug_occupancy": (ctypes.c_int, [P, P, P]),
+        "vmp_debug_quiet_violations": (ctypes.c_int, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name, None)

@@ -233,3 +233,27 @@ class BatchedVmEnv:
         r = self._empty((self.n_envs,), torch.int64)
         check(lib().vmp_get_rank(h, ptr(r)))
         return r
+
+    # ------------------------------------------------- checkpoint / resume
+    def snapshot(self):
+        """The whole batched env state (vmp_snapshot: PCG64 streams, counters,
+        PM and VM words) as a device u8 tensor; `restore` on an env of the same
+        config and n_envs continues bit-exactly from here. torch.save it for a
+        resumable run."""
+        h = self._bind()
+        n = ctypes.c_int64()
+        check(lib().vmp_snapshot_bytes(h, ctypes.byref(n)))
+        buf = self._empty((n.value,), torch.uint8)
+        check(lib().vmp_snapshot(h, ptr(buf)))
+        return buf
+
+    def restore(self, snap):
+        """Load a `snapshot()` (any device or host tensor) into this env."""
+        h = self._bind()
+        s = torch.as_tensor(snap).to(device=self.device, dtype=torch.uint8).contiguous()
+        n = ctypes.c_int64()
+        check(lib().vmp_snapshot_bytes(h, ctypes.byref(n)))
+        if s.numel() != n.value:
+            raise ValueError(f"snapshot holds {s.numel()} bytes, this env needs {n.value}")
+        check(lib().vmp_restore(h, ptr(s)))
+        torch.cuda.current_stream(self.device).synchronize()  # s may be a temporary copy

@@ -241,15 +241,37 @@ def actor_head_bf16_supported(K, A):
     return K % 64 == 0 and A <= ACTOR_HEAD_MAX_A
 
 
+def _bf16_operands(hb, wb, bias, V, A, bits, action, who):
+    """Shape / dtype / layout contract of vmp_actor_head_bf16_fwd/_bwd
+    (include/vmp.h): contiguous bf16 h [B, K] and weight [V*A, K], 16-byte
+    aligned; f32 bias [V*A]; mask bits contiguous int32 [B, V, ceil(A/32)]
+    with 16-byte aligned rows of the vector loads; actions as contiguous
+    int32 [B, V] (cast here, as the forward always did)."""
+    _need_device(hb, who)
+    if hb.dim() != 2 or hb.dtype != torch.bfloat16 or not hb.is_contiguous():
+        raise ValueError(f"{who}: h must be contiguous bf16 [B, K]")
+    B, K = hb.shape
+    if (tuple(wb.shape) != (V * A, K) or wb.dtype != torch.bfloat16 or not wb.is_contiguous()):
+        raise ValueError(f"{who}: weight must be contiguous bf16 [{V * A}, {K}]")
+    if (hb.data_ptr() | wb.data_ptr()) & 15:
+        raise ValueError(f"{who}: h and weight must be 16-byte aligned")
+    if bias.numel() != V * A or bias.dtype != torch.float32:
+        raise ValueError(f"{who}: bias must be f32 [{V * A}]")
+    if bits is not None:
+        if (tuple(bits.shape) != (B, V, (A + 31) // 32) or bits.dtype != torch.int32
+                or not bits.is_contiguous()):
+            raise ValueError(f"{who}: mask bits must be contiguous int32 {(B, V, (A + 31) // 32)}")
+        if bits.data_ptr() & 15:
+            raise ValueError(f"{who}: mask bits must be 16-byte aligned")
+    act = action.to(device=hb.device, dtype=torch.int32).reshape(B, V).contiguous()
+    return B, K, act
+
+
 def actor_head_bf16_fwd(hb, wb, bias, V, A, bits, action):
     """The bf16 training forward (vmp_actor_head_bf16_fwd): hb bf16 [B, K], wb bf16
     [V*A, K], bias f32 [V*A], GIVEN actions -> (logprob [B], entropy [B]); the
     logits are consumed in registers, never written."""
-    _need_device(hb, "actor_head_bf16_fwd")
-    B, K = hb.shape
-    if bits is not None and tuple(bits.shape) != (B, V, (A + 31) // 32):
-        raise ValueError(f"mask bits {tuple(bits.shape)} != {(B, V, (A + 31) // 32)}")
-    act = action.to(device=hb.device, dtype=torch.int32).reshape(B, V).contiguous()
+    B, K, act = _bf16_operands(hb, wb, bias, V, A, bits, action, "actor_head_bf16_fwd")
     lp = torch.empty((B,), dtype=torch.float32, device=hb.device)
     ent = torch.empty((B,), dtype=torch.float32, device=hb.device)
     ws = torch.empty((2 * B * V,), dtype=torch.float32, device=hb.device)
@@ -263,14 +285,16 @@ def actor_head_bf16_bwd(hb, wb, bias, V, A, bits, action, g_lp, g_ent, out):
     """The bf16 training backward (vmp_actor_head_bf16_bwd) over the rows of hb
     (a chunk): recomputes the logits tiles and writes bf16 dlogits into `out`
     ([rows, >= V*A], row stride out.stride(0))."""
-    _need_device(hb, "actor_head_bf16_bwd")
-    B, K = hb.shape
-    if out.dtype != torch.bfloat16 or out.shape[0] < B or out.stride(1) != 1:
-        raise ValueError("dlogits out must be bf16 [rows, V*A] with unit column stride")
+    B, K, act = _bf16_operands(hb, wb, bias, V, A, bits, action, "actor_head_bf16_bwd")
+    if (out.dtype != torch.bfloat16 or out.dim() != 2 or out.shape[0] < B
+            or out.shape[1] < V * A or out.stride(1) != 1):
+        raise ValueError("dlogits out must be bf16 [rows, >= V*A] with unit column stride")
+    if out.data_ptr() & 3:
+        raise ValueError("dlogits out must be 4-byte aligned")
     glp = None if g_lp is None else g_lp.float().contiguous()
     gen = None if g_ent is None else g_ent.float().contiguous()
     check(lib().vmp_actor_head_bf16_bwd(B, K, V, A, ptr(hb), ptr(wb), ptr(bias.contiguous()),
-                                        ptr(bits), ptr(action), ptr(glp), ptr(gen), ptr(out),
+                                        ptr(bits), ptr(act), ptr(glp), ptr(gen), ptr(out),
                                         int(out.stride(0)), _stream(hb)))
     return out
 

@@ -68,6 +68,8 @@ class PPOConfig:
     precision: str = "f32"             # "bf16": bf16 GEMM inputs, f32 accumulate/output
     chunk_bytes: int = 0               # logits budget per update chunk (0: from free HBM, fixed at the first update)
     dlogits_chunk_bytes: int = 1 << 32  # bf16 fused head: dlogits rows per backward chunk
+    kl_lookahead: bool = True          # step before the KL early-stop flag reaches the host,
+                                       # roll back on a break (same accepted steps)
     seed_stride: int = 4               # env/episode reset seed spacing
 
 
@@ -231,6 +233,24 @@ class BF16FusedActorHead(torch.autograd.Function):
         return gx, gw, gb, None, None, None, None, None
 
 
+def _host_scalar(t):
+    """Start copying a one-element device tensor to the host now and return a
+    callable that waits for that copy alone (an event, not a device sync) and
+    gives the value as a Python float."""
+    if not t.is_cuda:
+        v = float(t.reshape(-1)[0])
+        return lambda: v
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+
+    def read():
+        ev.synchronize()
+        return float(h.reshape(-1)[0])
+    return read
+
+
 def _run_mlp(seq, x, precision):
     if precision != "bf16":
         return seq(x)
@@ -328,9 +348,15 @@ class Network(nn.Module):
                 and H.actor_head_bf16_supported(last.in_features, self.A))
 
     def logits_bytes_per_sample(self):
-        """HBM the update's head needs per sample beyond activations: the f32
-        logits (and their gradient) of the logits paths; ~0 on the fused one."""
-        return 0 if self.bf16_fused() else 4 * self.V * self.A
+        """HBM the update holds per sample of a chunk: the activations the MLPs
+        keep for backward (per hidden layer of actor and critic the f32
+        pre-activation and tanh output and, in bf16, the GEMM input copy:
+        <= 10 H bytes, 4 layers) plus the head's own: the f32 logits of the
+        logits paths, or the fused head's 2 V f32 row workspace (its dlogits
+        are bounded separately by dlogits_chunk_bytes)."""
+        H = int(self.actor[0].out_features)
+        head = 8 * self.V if self.bf16_fused() else 4 * self.V * self.A
+        return head + 40 * H
 
     def logprob_entropy(self, obs, bits, action, dlogits_chunk_bytes=1 << 32):
         """get_action(obs, action, mask)'s logprob and entropy (ppo.py:115-126) for
@@ -683,82 +709,163 @@ class PPOTrainer:
             adv, ret = self.gae(rew, done, values, next_values, cfg.gamma, cfg.lamda)
         mbs = int(cfg.minibatch_size)
         n_mb = math.ceil(T / mbs)
-        eps = cfg.eps_clip
         params = [p for p in m.parameters()]
-        stats = dict(minibatches=0, kl_breaks=0, clipfracs=[])
+        stats = dict(minibatches=0, kl_breaks=0, clipfracs=[], rollbacks=0)
         clipfracs = []  # device scalars, read once after the update (no per-minibatch sync)
-        for epoch in range(cfg.k_epochs):
-            for j in range(n_mb):
-                t0, t1 = j * mbs, min(T, (j + 1) * mbs)
-                mt = t1 - t0
-                m_glob = mt * N * self.world
-                with torch.no_grad():
-                    a_mb = adv[t0:t1]
-                    s = self._allreduce(a_mb.sum().reshape(1).double())
-                    mean = (s / m_glob).float()
-                    ss = self._allreduce(((a_mb - mean) ** 2).sum().reshape(1).double())
-                    std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
-                    adv_n = (a_mb - mean) / (std + 1e-10)
-                per_env = mt * m.logits_bytes_per_sample()
-                ce = N if per_env == 0 else max(1, min(N, self._chunk_budget(rew.device) // per_env))
-                self._zero_grads(params)
-                kl_sum = torch.zeros(1, dtype=torch.float64, device=rew.device)
-                clip_n = torch.zeros(1, dtype=torch.float64, device=rew.device)
-                for n0 in range(0, N, ce):
-                    n1 = min(N, n0 + ce)
-                    nc = n1 - n0
-                    o = obs[t0:t1, n0:n1].reshape(mt * nc, -1)
-                    b = None if bits is None else bits[t0:t1, n0:n1].reshape(mt * nc, self.V, -1)
-                    a = act[t0:t1, n0:n1].reshape(mt * nc, self.V)
-                    newlp, ent = m.logprob_entropy(o, b, a, cfg.dlogits_chunk_bytes)
-                    newlp = newlp.reshape(mt, nc)
-                    logratio = newlp - old_lp[t0:t1, n0:n1]
-                    ratio = torch.exp(logratio)
-                    kl_sum += logratio.detach().double().sum()
-                    clip_n += ((ratio.detach() - 1.0).abs() > eps).double().sum()
-                    an = adv_n[:, n0:n1]
-                    surr = -ratio * an
-                    surr_c = -torch.clamp(ratio, 1 - eps, 1 + eps) * an
-                    loss_clip = torch.max(surr, surr_c).sum() / m_glob
-                    newv = m.get_value(o).reshape(mt, nc)
-                    R, Vb = ret[t0:t1, n0:n1], values[t0:t1, n0:n1]
-                    if cfg.value_loss_broadcast:
-                        # newvalues [mb,1] - returns [mb] -> [mb, mb] (ppo.py:266-270), per env
-                        du = newv[:, None, :] - R[None, :, :]
-                        vcl = Vb[None, :, :] + torch.clamp(newv[:, None, :] - Vb[None, :, :],
-                                                           -eps, eps)
-                        dc = vcl - R[None, :, :]
-                        denom = mt * mt * N * self.world
-                    else:
-                        du = newv - R
-                        dc = Vb + torch.clamp(newv - Vb, -eps, eps) - R
-                        denom = m_glob
-                    if cfg.vf_loss_clip:
-                        lvf = torch.max(du * du, dc * dc).sum() / denom
-                    else:
-                        lvf = (du * du).sum() / denom
-                    loss = loss_clip - cfg.ent_coef * ent.sum() / m_glob + cfg.vf_coef * 0.5 * lvf
-                    loss.backward()
-                self._allreduce(kl_sum)
+        batch = (obs, bits, act, old_lp, values, adv, ret, N)
+
+        def after(pos):  # the reference's loop order: minibatches of an epoch, epochs
+            e, j = pos
+            return (e, j + 1) if j + 1 < n_mb else ((e + 1, 0) if e + 1 < cfg.k_epochs else None)
+
+        if not cfg.kl_lookahead:
+            pos = (0, 0) if cfg.k_epochs > 0 and n_mb > 0 else None
+            while pos is not None:
+                kl_sum, clip_n, m_glob = self._minibatch_backward(batch, pos[1] * mbs,
+                                                                  min(T, (pos[1] + 1) * mbs))
                 # the one host sync per minibatch: the reference's loop control
                 # (ppo.py:263-264) decides on the host whether this minibatch steps
                 kl = float(-kl_sum / m_glob)
                 if kl > cfg.kl_max:  # ppo.py:263-264: leaves this epoch's minibatch loop
                     self._zero_grads(params)
                     stats["kl_breaks"] += 1
-                    break
-                self._allreduce(clip_n)
-                clipfracs.append(clip_n / m_glob)
-                if self.dist:  # the grads are views of one flat buffer: one all-reduce
-                    self.dist.all_reduce(self._gflat, group=self.group)
-                nn.utils.clip_grad_norm_(params, cfg.max_grad_norm)
-                self.agent.optimizer.step()
+                    pos = (pos[0] + 1, 0) if pos[0] + 1 < cfg.k_epochs else None
+                    continue
+                clipfracs.append(self._optimizer_step(params, clip_n, m_glob))
                 stats["minibatches"] += 1
                 stats["kl"] = kl
+                pos = after(pos)
+        else:
+            # KL look-ahead: minibatch i's optimizer step is taken before its KL is
+            # known on the host, and minibatch i + 1 is enqueued behind it; the
+            # host reads KL_i while the device runs i + 1. If KL_i breaks the
+            # epoch (ppo.py:263-264), the parameters and AdamW state go back to
+            # the copy taken before step i and minibatch i + 1 is discarded: the
+            # accepted steps are the reference's sequence, bit for bit, without a
+            # drained queue at every minibatch.
+            inflight = None
+            pos = (0, 0) if cfg.k_epochs > 0 and n_mb > 0 else None
+            while pos is not None or inflight is not None:
+                cur = None
+                if pos is not None:
+                    snap = self._opt_snapshot(params)
+                    kl_sum, clip_n, m_glob = self._minibatch_backward(
+                        batch, pos[1] * mbs, min(T, (pos[1] + 1) * mbs))
+                    kl_host = _host_scalar(kl_sum)
+                    cf = self._optimizer_step(params, clip_n, m_glob)
+                    cur = dict(pos=pos, kl=kl_host, m_glob=m_glob, snap=snap, cf=cf)
+                    pos = after(pos)
+                if inflight is not None:
+                    kl = -inflight["kl"]() / inflight["m_glob"]
+                    if kl > cfg.kl_max:
+                        self._opt_restore(params, inflight["snap"])
+                        stats["kl_breaks"] += 1
+                        stats["rollbacks"] += 1 + (cur is not None)
+                        e = inflight["pos"][0]
+                        pos = (e + 1, 0) if e + 1 < cfg.k_epochs else None
+                        cur = None
+                    else:
+                        clipfracs.append(inflight["cf"])
+                        stats["minibatches"] += 1
+                        stats["kl"] = kl
+                inflight = cur
         if clipfracs:
             stats["clipfracs"] = torch.cat(clipfracs).double().cpu().tolist()
         self.stats = stats
         return stats
+
+    def _minibatch_backward(self, batch, t0, t1):
+        """Loss of time slice [t0, t1) of every env (ppo.py:250-287), backward into
+        the parameters' grads -> (kl_sum, clip count) device f64 [1] (KL sum
+        all-reduced), and the global sample count."""
+        obs, bits, act, old_lp, values, adv, ret, N = batch
+        cfg, m = self.cfg, self.model
+        eps = cfg.eps_clip
+        params = [p for p in m.parameters()]
+        mt = t1 - t0
+        m_glob = mt * N * self.world
+        dev = adv.device
+        with torch.no_grad():
+            a_mb = adv[t0:t1]
+            s = self._allreduce(a_mb.sum().reshape(1).double())
+            mean = (s / m_glob).float()
+            ss = self._allreduce(((a_mb - mean) ** 2).sum().reshape(1).double())
+            std = torch.sqrt(ss / max(m_glob - 1, 1)).float()
+            adv_n = (a_mb - mean) / (std + 1e-10)
+        per_env = mt * m.logits_bytes_per_sample()
+        ce = max(1, min(N, self._chunk_budget(dev) // per_env))
+        self._zero_grads(params)
+        kl_sum = torch.zeros(1, dtype=torch.float64, device=dev)
+        clip_n = torch.zeros(1, dtype=torch.float64, device=dev)
+        for n0 in range(0, N, ce):
+            n1 = min(N, n0 + ce)
+            nc = n1 - n0
+            o = obs[t0:t1, n0:n1].reshape(mt * nc, -1)
+            b = None if bits is None else bits[t0:t1, n0:n1].reshape(mt * nc, self.V, -1)
+            a = act[t0:t1, n0:n1].reshape(mt * nc, self.V)
+            newlp, ent = m.logprob_entropy(o, b, a, cfg.dlogits_chunk_bytes)
+            newlp = newlp.reshape(mt, nc)
+            logratio = newlp - old_lp[t0:t1, n0:n1]
+            ratio = torch.exp(logratio)
+            kl_sum += logratio.detach().double().sum()
+            clip_n += ((ratio.detach() - 1.0).abs() > eps).double().sum()
+            an = adv_n[:, n0:n1]
+            surr = -ratio * an
+            surr_c = -torch.clamp(ratio, 1 - eps, 1 + eps) * an
+            loss_clip = torch.max(surr, surr_c).sum() / m_glob
+            newv = m.get_value(o).reshape(mt, nc)
+            R, Vb = ret[t0:t1, n0:n1], values[t0:t1, n0:n1]
+            if cfg.value_loss_broadcast:
+                # newvalues [mb,1] - returns [mb] -> [mb, mb] (ppo.py:266-270), per env
+                du = newv[:, None, :] - R[None, :, :]
+                vcl = Vb[None, :, :] + torch.clamp(newv[:, None, :] - Vb[None, :, :], -eps, eps)
+                dc = vcl - R[None, :, :]
+                denom = mt * mt * N * self.world
+            else:
+                du = newv - R
+                dc = Vb + torch.clamp(newv - Vb, -eps, eps) - R
+                denom = m_glob
+            if cfg.vf_loss_clip:
+                lvf = torch.max(du * du, dc * dc).sum() / denom
+            else:
+                lvf = (du * du).sum() / denom
+            loss = loss_clip - cfg.ent_coef * ent.sum() / m_glob + cfg.vf_coef * 0.5 * lvf
+            loss.backward()
+        self._allreduce(kl_sum)
+        return kl_sum, clip_n, m_glob
+
+    def _optimizer_step(self, params, clip_n, m_glob):
+        """Clip fraction all-reduce, gradient all-reduce (data parallel), grad-norm
+        clipping and the AdamW step (ppo.py:283-287) -> the clip fraction
+        (device scalar)."""
+        self._allreduce(clip_n)
+        if self.dist:  # the grads are views of one flat buffer: one all-reduce
+            self.dist.all_reduce(self._gflat, group=self.group)
+        nn.utils.clip_grad_norm_(params, self.cfg.max_grad_norm)
+        self.agent.optimizer.step()
+        return clip_n / m_glob
+
+    def _opt_snapshot(self, params):
+        """Device copies of the parameters and of AdamW's per-parameter state
+        (its host `step` counters too) before a look-ahead step."""
+        opt = self.agent.optimizer
+        with torch.no_grad():
+            ps = [p.detach().clone() for p in params]
+            st = [{k: v.clone() for k, v in opt.state[p].items()} if p in opt.state else None
+                  for p in params]
+        return ps, st
+
+    def _opt_restore(self, params, snap):
+        opt = self.agent.optimizer
+        ps, st = snap
+        with torch.no_grad():
+            for p, c, s in zip(params, ps, st):
+                p.copy_(c)  # bumps p._version: the bf16 weight copies re-cast
+                if s is None:
+                    opt.state.pop(p, None)
+                else:
+                    for k, v in s.items():
+                        opt.state[p][k].copy_(v)
 
     def _chunk_budget(self, dev):
         """The update's chunk budget, fixed once per trainer (the chunk count sets
