@@ -128,7 +128,7 @@ struct vmp_handle {
   int32_t device;
   int32_t eval_mode;
   hipStream_t stream;
-  uint64_t *vmw;
+  uint32_t *vmw;  // [N][vm_pitch(V)]
   double *pm;
   EnvHdr *hdr;
   double *lg_arr, *lg_svc;
@@ -435,7 +435,7 @@ int vmp_create(const vmp_config *cfg, int32_t n_env, const int64_t *seeds, int32
 // vmp_create after the handle exists: every failure returns a code and the
 // caller destroys the handle (vmp_destroy tolerates what was not allocated).
 static int create_rest(vmp_handle *h, const vmp_config *cfg, int32_t n_env, const int64_t *seeds) {
-  hipError_t e1 = dev_malloc(&h->vmw, sizeof(uint64_t) * (size_t)n_env * h->V);
+  hipError_t e1 = dev_malloc(&h->vmw, sizeof(uint32_t) * (size_t)n_env * vm_pitch(h->V));
   hipError_t e2 = dev_malloc(&h->pm, sizeof(double) * (size_t)n_env * 2 * h->P);
   hipError_t e3 = dev_malloc(&h->hdr, sizeof(EnvHdr) * (size_t)n_env);
   if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
@@ -830,7 +830,7 @@ int vmp_get_rank(vmp_handle *h, int64_t *rank) {
 }
 
 // ---- checkpoint / resume of the batched env state ----
-// Snapshot = a 256-B descriptor, then hdr[N] | pm[N][2P] | vmw[N][V] as the
+// Snapshot = a 256-B descriptor, then hdr[N] | pm[N][2P] | vmw[N][pitch] as the
 // kernels keep them (PCG64 states, sequence bases, counters, step hints and
 // finish keys included), so a restore is bit-exact by construction: the
 // restored handle holds the very bytes every later kernel reads.
@@ -846,7 +846,7 @@ struct SnapDesc {
 static_assert(sizeof(SnapDesc) <= kSnapHead, "snapshot descriptor exceeds its header");
 int64_t snap_bytes(const vmp_handle *h) {
   return kSnapHead + (int64_t)sizeof(EnvHdr) * h->N + 16 * (int64_t)h->N * h->P +
-         8 * (int64_t)h->N * h->V;
+         4 * (int64_t)h->N * vm_pitch(h->V);
 }
 bool same_config(const vmp_config &a, const vmp_config &b) {
   vmp_config x = a, y = b;
@@ -879,7 +879,7 @@ int vmp_snapshot(vmp_handle *h, void *dst) {
   HIP_TRY(hipMemcpyAsync(o, head, kSnapHead, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(o + kSnapHead, h->hdr, nh, hipMemcpyDeviceToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(o + kSnapHead + nh, h->pm, np, hipMemcpyDeviceToDevice, h->stream));
-  HIP_TRY(hipMemcpyAsync(o + kSnapHead + nh + np, h->vmw, 8 * (size_t)h->N * h->V,
+  HIP_TRY(hipMemcpyAsync(o + kSnapHead + nh + np, h->vmw, 4 * (size_t)h->N * vm_pitch(h->V),
                          hipMemcpyDeviceToDevice, h->stream));
   // the descriptor's host copy is a stack buffer: the call returns after it is read
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -900,7 +900,7 @@ int vmp_restore(vmp_handle *h, const void *src) {
   const size_t nh = sizeof(EnvHdr) * (size_t)h->N, np = 16 * (size_t)h->N * h->P;
   HIP_TRY(hipMemcpyAsync(h->hdr, s + kSnapHead, nh, hipMemcpyDeviceToDevice, h->stream));
   HIP_TRY(hipMemcpyAsync(h->pm, s + kSnapHead + nh, np, hipMemcpyDeviceToDevice, h->stream));
-  HIP_TRY(hipMemcpyAsync(h->vmw, s + kSnapHead + nh + np, 8 * (size_t)h->N * h->V,
+  HIP_TRY(hipMemcpyAsync(h->vmw, s + kSnapHead + nh + np, 4 * (size_t)h->N * vm_pitch(h->V),
                          hipMemcpyDeviceToDevice, h->stream));
   return VMP_OK;
 }

@@ -1533,7 +1533,7 @@ template <int VPT, bool LAZY>
 __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, const Tables &T,
                                            uint32_t (&wa)[VPT], uint32_t (&rem)[VPT],
                                            uint32_t run0, uint32_t fb, uint32_t &dirty,
-                                           uint64_t *vmo, int kstep, bool ext,
+                                           uint32_t *vmo, int kstep, bool ext,
                                            bool quiet_in, bool &terminated, bool &calm,
                                            bool &has_ex STAMP_PARAMS) {
   const int lane = lane_id();
@@ -1627,7 +1627,8 @@ __device__ __forceinline__ double env_tail(const EnvParams &p, const Lds &L, con
           if (s == (v >> 6)) {
             wa[s] = w_make(WAIT, cc, cm);
             if (LAZY) {  // final for this launch: stored now, skipped at the end
-              ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rr << 32));
+              ST_NT(vmo + vm_slot_idx(v), wa[s]);
+              ST_NT(vmo + vm_time_idx(v), rr);
               dirty &= ~(1u << s);
             } else {
               rem[s] = rr;
@@ -1874,23 +1875,21 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
 #pragma unroll
   for (int j = 0; j < 4; j++) pv[j] = pm[min(j * 64 + lane, n_pm - 1)];
   __asm__ volatile("" ::: "memory");  // keep the issue order: header/PM first
-  const uint64_t *vmw = p.vmw + (int64_t)e * V;
-  // ONE: only the low halves (placement, sizes) go to registers here; the
+  // ONE: only the slot words (placement, sizes) go to registers here; the
   // finish keys are read after the draws and folded into one bit per slot
-  const uint32_t GLBP *vlo = gptr(reinterpret_cast<const uint32_t *>(vmw));
+  // (slot and time words sit in separate 256-B runs of each 64-slot block)
+  const uint32_t GLBP *vlo = gptr(p.vmw + (int64_t)e * vm_pitch(V));
   uint32_t wa[VPT], rem[VPT];
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
+    const uint32_t x = vlo[vm_slot_idx(min(v, V - 1))];
+    wa[s] = v < V ? x : (uint32_t)kPad;
     if (ONE) {
-      const uint32_t x = vlo[2 * min(v, V - 1)];
-      wa[s] = v < V ? x : (uint32_t)kPad;
       rem[s] = 0;
     } else {
-      const uint64_t x = vmw[min(v, V - 1)];
-      const uint64_t w = v < V ? x : (uint64_t)kPad;
-      wa[s] = (uint32_t)w;
-      rem[s] = (uint32_t)(w >> 32);
+      const uint32_t y = vlo[vm_time_idx(min(v, V - 1))];
+      rem[s] = v < V ? y : 0u;
     }
   }
   __asm__ volatile("" ::: "memory");  // ... and the VM words before any wait
@@ -1951,10 +1950,10 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   if (ONE && !EXT) {
     // issued before the action phase, consumed after it (latency hidden by it)
 #pragma unroll
-    for (int s = 0; s < VPT; s++) hiv[s] = vlo[2 * min(s * 64 + lane, V - 1) + 1];
+    for (int s = 0; s < VPT; s++) hiv[s] = vlo[vm_time_idx(min(s * 64 + lane, V - 1))];
     __asm__ volatile("" ::: "memory");
   }
-  uint64_t *vmo = p.vmw + (int64_t)e * V;
+  uint32_t *vmo = p.vmw + (int64_t)e * vm_pitch(V);
   const int k_steps = ONE ? 1 : o.k_steps;
   // EnvHdr::pad bit 62 (see heuristic_apply); the external-action kernel
   // neither uses nor keeps it
@@ -1980,7 +1979,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
       if (ONE) {
         const int ln = fresh_lane();
 #pragma unroll
-        for (int s = 0; s < VPT; s++) hiv[s] = vlo[2 * min(s * 64 + ln, V - 1) + 1];
+        for (int s = 0; s < VPT; s++) hiv[s] = vlo[vm_time_idx(min(s * 64 + ln, V - 1))];
       }
     }
     STAMP(1);
@@ -2043,14 +2042,16 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
       const int v = s * 64 + ln;
       if (live(wa[s]) && ((dirty >> s) & 1u)) {  // unchanged words stay as they are
         if (!ONE) {
-          ST_NT(vmo + v, (uint64_t)wa[s] | ((uint64_t)rem[s] << 32));
+          ST_NT(vmo + vm_slot_idx(v), wa[s]);
+          ST_NT(vmo + vm_time_idx(v), rem[s]);
         } else if (w_pl(wa[s]) == P + 1) {  // finished: NULL, remaining 0
-          ST_NT(vmo + v, (uint64_t)wa[s]);
+          ST_NT(vmo + vm_slot_idx(v), wa[s]);
+          ST_NT(vmo + vm_time_idx(v), 0u);
         } else {  // placed (r -> F = t + r) or suspended (F -> r = F - t)
-          uint32_t GLBP *w32 = gptr(reinterpret_cast<uint32_t *>(vmo + v));
-          w32[0] = wa[s];
-          __hip_atomic_fetch_add(w32 + 1, w_pl(wa[s]) < P ? t32 : 0u - t32, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+          uint32_t GLBP *w32 = gptr(vmo);
+          w32[vm_slot_idx(v)] = wa[s];
+          __hip_atomic_fetch_add(w32 + vm_time_idx(v), w_pl(wa[s]) < P ? t32 : 0u - t32,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
@@ -2153,8 +2154,11 @@ __global__ __launch_bounds__(256) void k_reset(EnvParams p, const int64_t *seeds
   if (lane >= 20 && lane < 32) {
     reinterpret_cast<uint64_t *>(h)[lane] = (lane == 20) ? 1ull : 0ull;  // timestep = 1
   }
-  uint64_t nul = (uint64_t)(P + 1);
-  for (int v = lane; v < V; v += 64) p.vmw[(int64_t)e * V + v] = nul;
+  uint32_t *vw = p.vmw + (int64_t)e * vm_pitch(V);
+  for (int v = lane; v < V; v += 64) {
+    vw[vm_slot_idx(v)] = (uint32_t)(P + 1);
+    vw[vm_time_idx(v)] = 0u;
+  }
   for (int i = lane; i < 2 * P; i += 64) p.pm[(int64_t)e * 2 * P + i] = 0.0;
   if (obs) {
     float *o = obs + (int64_t)e * p.D;
@@ -2168,7 +2172,9 @@ __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t nv = (int64_t)p.N * p.V;
   if (i < nv) {
-    uint64_t w = p.vmw[i];
+    const uint32_t *vw = p.vmw + (i / p.V) * vm_pitch(p.V);
+    const int v = (int)(i % p.V);
+    const uint64_t w = (uint64_t)vw[vm_slot_idx(v)] | ((uint64_t)vw[vm_time_idx(v)] << 32);
     if (placement) placement[i] = (int64_t)(w & 0xFFFF);
     if (vm_cpu) vm_cpu[i] = (double)((w >> 16) & 0xFF) / 100.0;
     if (vm_mem) vm_mem[i] = (double)((w >> 24) & 0xFF) / 100.0;
@@ -2185,10 +2191,10 @@ __global__ void k_export(EnvParams p, int64_t *placement, double *vm_cpu, double
   }
   if (rank && i < p.N) {  // _get_rank (env.py:320-325): distinct PMs hosting a VM
     int64_t r = 0;
-    const uint64_t *row = p.vmw + i * p.V;
+    const uint32_t *row = p.vmw + i * vm_pitch(p.V);
     for (int q = 0; q < p.P; q++) {
       bool used = false;
-      for (int v = 0; v < p.V && !used; v++) used = (int)(row[v] & 0xFFFF) == q;
+      for (int v = 0; v < p.V && !used; v++) used = (int)(row[vm_slot_idx(v)] & 0xFFFF) == q;
       r += used;
     }
     rank[i] = r;
@@ -2210,12 +2216,12 @@ __global__ __launch_bounds__(256) void k_target_means(EnvParams p) {
   const int e = uni(blockIdx.x * kWavesPerBlock + wid);
   if (e >= p.N) return;
   const int V = p.V, P = p.P;
-  const uint64_t *row = p.vmw + (int64_t)e * V;
+  const uint32_t *row = p.vmw + (int64_t)e * vm_pitch(V);
   uint8_t *cc = comp[wid][0], *cm = comp[wid][1];
   int n_ex = 0;
   for (int b = 0; b < V; b += 64) {
     const int v = b + lane;
-    const uint64_t w = v < V ? row[v] : (uint64_t)(P + 1);
+    const uint32_t w = v < V ? row[vm_slot_idx(v)] : (uint32_t)(P + 1);
     const bool ex = v < V && (int)(w & 0xFFFFu) <= P;
     const uint64_t m = ballot(ex);
     if (ex) {
@@ -3030,7 +3036,7 @@ __device__ __forceinline__ void big_store(const EnvParams &p, const Lds &L, cons
                                           bool state, int e) {
   const int t = threadIdx.x, NT = kBigNT;
   const int V = p.V, P = p.P;
-  uint32_t *vmo = reinterpret_cast<uint32_t *>(p.vmw + (int64_t)e * V);
+  uint32_t *vmo = p.vmw + (int64_t)e * vm_pitch(V);
 VMP_SLOOP
   for (int s = 0; s < SPT; s++) {
     const int v = s * NT + t;
@@ -3041,7 +3047,7 @@ VMP_SLOOP
         ST_NT(obs + V + v, T.fcent[w_cc(w)]);
         ST_NT(obs + 2 * V + v, T.fcent[w_cm(w)]);
       }
-      if (state && ((dirty >> s) & 1u)) ST_NT(vmo + 2 * v, w);
+      if (state && ((dirty >> s) & 1u)) ST_NT(vmo + vm_slot_idx(v), w);
     }
   }
   if (obs)
@@ -3063,10 +3069,10 @@ __device__ __forceinline__ void big_store_words(const EnvParams &p, const Lds &L
                                                 SMask dirty, int e) {
   const int t = threadIdx.x, NT = kBigNT;
   const int V = p.V, P = p.P;
-  uint32_t *vmo = reinterpret_cast<uint32_t *>(p.vmw + (int64_t)e * V);
+  uint32_t *vmo = p.vmw + (int64_t)e * vm_pitch(V);
 #pragma unroll
   for (int s = 0; s < SPT; s++)
-    if (((dirty >> s) & 1u) && live(wr[s])) ST_NT(vmo + 2 * (s * NT + t), wr[s]);
+    if (((dirty >> s) & 1u) && live(wr[s])) ST_NT(vmo + vm_slot_idx(s * NT + t), wr[s]);
   double *pmo = p.pm + (int64_t)e * 2 * P;
   for (int i = t; i < 2 * P; i += NT)
     if ((L.pdirty[i >> 6] >> (i & 63)) & 1ull) ST_NT(pmo + i, (double)L.cpu[i]);
@@ -3140,7 +3146,7 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
   const bool w0 = t < 64;
   const int P = p.P, WAIT = p.P, NUL = p.P + 1;
   EnvHdr LDSP *H = L.hdr;
-  uint32_t *vw32 = reinterpret_cast<uint32_t *>(p.vmw + (int64_t)e * p.V);
+  uint32_t *vw32 = p.vmw + (int64_t)e * vm_pitch(p.V);
   // ---- _run_vms: finish keys (env_tail), then free the finishers in ascending VM order ----
   const uint32_t t32 = (uint32_t)H->timestep;
   SMask fterm = 0;
@@ -3162,7 +3168,7 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
   {
     uint32_t hw[SPT];  // the time words, issued together, dead after this loop
 #pragma unroll
-    for (int s = 0; s < SPT; s++) hw[s] = gptr(vw32)[2 * min(s * NT + t, p.V - 1) + 1];
+    for (int s = 0; s < SPT; s++) hw[s] = gptr(vw32)[vm_time_idx(min(s * NT + t, p.V - 1))];
 #pragma unroll
     for (int s = 0; s < SPT; s++) {
       const int v = s * NT + t;
@@ -3176,7 +3182,7 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
         fterm |= SBIT(s);
         h = 0;  // the word becomes NULL (below)
       }
-      if (h != hw[s]) ST_NT(vw32 + 2 * v + 1, h);  // padded slots never change
+      if (h != hw[s]) ST_NT(vw32 + vm_time_idx(v), h);  // padded slots never change
     }
   }
   dirty |= fterm;
@@ -3287,7 +3293,7 @@ VMP_SLOOP
 #ifdef VMP_BIG_REG_WR
           W[s * NT + t] = wr[s];
 #endif
-          ST_NT(vw32 + 2 * (s * NT + t) + 1, (uint32_t)L.evt[j - j0]);
+          ST_NT(vw32 + vm_time_idx(s * NT + t), (uint32_t)L.evt[j - j0]);
           dirty |= SBIT(s);
         }
       }
@@ -3426,7 +3432,7 @@ __global__ __launch_bounds__(kBigNT, ONE ? VMP_BIG_WPE_ONE : 2) void k_env_big(E
   double pv[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) pv[j] = pm[min(j * NT + t, n_pm - 1)];
-  const uint64_t GLBP *vmw = gptr(p.vmw + (int64_t)e * V);
+  const uint32_t GLBP *vmw = gptr(p.vmw + (int64_t)e * vm_pitch(V));
   __asm__ volatile("" ::: "memory");
   if (t < 32) reinterpret_cast<uint64_t LDSP *>(L.hdr)[t] = hv;
   if (w0) {
@@ -3441,10 +3447,9 @@ __global__ __launch_bounds__(kBigNT, ONE ? VMP_BIG_WPE_ONE : 2) void k_env_big(E
     // the time words are read by big_tail
     constexpr int kLd = kBigNT - 64, kLPT = (SPT * kBigNT + kLd - 1) / kLd;
     const int tl = t - 64;
-    const uint32_t GLBP *vw32 = reinterpret_cast<const uint32_t GLBP *>(vmw);
     uint32_t wl[kLPT];
 #pragma unroll
-    for (int j = 0; j < kLPT; j++) wl[j] = vw32[2 * min(j * kLd + tl, V - 1)];
+    for (int j = 0; j < kLPT; j++) wl[j] = vmw[vm_slot_idx(min(j * kLd + tl, V - 1))];
 #pragma unroll
     for (int j = 0; j < kLPT; j++) {
       const int v = j * kLd + tl;
@@ -3497,7 +3502,7 @@ VMP_SLOOP
   if (o.k_steps == 0 && o.policy >= 0 && o.act_out) {
     big_heuristic<SPT>(p, L, T, B, W, o.policy, o.act_out + (int64_t)e * V, nullptr STAMP_ARGS);
     __syncthreads();
-    for (int v = t; v < V; v += NT) W[v] = (uint32_t)vmw[v];  // act only: placements unchanged
+    for (int v = t; v < V; v += NT) W[v] = vmw[vm_slot_idx(v)];  // act only: placements unchanged
   }
   __syncthreads();
   STAMP(4);
@@ -3598,9 +3603,9 @@ __global__ __launch_bounds__(64) void k_rank(EnvParams p, int64_t *rank) {
   const int NWP = (p.P + 63) / 64;
   for (int i = lane; i < NWP; i += 64) used[i] = 0ull;
   __syncthreads();
-  const uint64_t *row = p.vmw + (int64_t)e * p.V;
+  const uint32_t *row = p.vmw + (int64_t)e * vm_pitch(p.V);
   for (int v = lane; v < p.V; v += 64) {
-    const int st = (int)(row[v] & 0xFFFFu);
+    const int st = (int)(row[vm_slot_idx(v)] & 0xFFFFu);
     if (st < p.P) atomicOr(used + (st >> 6), 1ull << (st & 63));
   }
   __syncthreads();
@@ -3621,11 +3626,11 @@ __global__ __launch_bounds__(64) void k_target_means_lds(EnvParams p) {
   const int lane = lane_id(), e = blockIdx.x;
   const Lds L = make_lds(p, (char LDSP *)lds);
   const int V = p.V, P = p.P;
-  const uint64_t *row = p.vmw + (int64_t)e * V;
+  const uint32_t *row = p.vmw + (int64_t)e * vm_pitch(V);
   int n_ex = 0;
   for (int b = 0; b < V; b += 64) {
     const int v = b + lane;
-    const uint64_t w = v < V ? row[v] : (uint64_t)(P + 1);
+    const uint32_t w = v < V ? row[vm_slot_idx(v)] : (uint32_t)(P + 1);
     const bool ex = v < V && (int)(w & 0xFFFFu) <= P;
     const uint64_t m = ballot(ex);
     if (ex) {

@@ -4,16 +4,22 @@
 // HBM layout, env-major so one wavefront streams one env's state with
 // coalesced 64-lane accesses (one wave per env):
 //
-//   vmw  u64 [N][V]   one word per VM slot (env.py:186-196 state, 8 B/VM):
-//                       bits  0..15 placement (0..P-1 PM, P = WAIT, P+1 = NULL)
-//                       bits 16..23 vm_cpu in hundredths (np.around(.,2) makes
-//                                   every size k/100 exactly, env.py:212-219)
-//                       bits 24..31 vm_memory in hundredths
-//                       bits 32..63 waiting VM: remaining runtime (env.py:290);
-//                                   running VM: finish key F = timestep +
-//                                   remaining, so a running VM's word does not
-//                                   change while it runs (the step kernels
-//                                   store only the words that changed)
+//   vmw  u32 [N][VB][2][64]  two 32-bit words per VM slot (env.py:186-196
+//                       state, 8 B/VM), in blocks of 64 slots (VB = ceil(V/64)):
+//                       block b holds the SLOT words of slots 64b..64b+63,
+//                       then their TIME words, so a kernel that reads only
+//                       one kind touches only that kind's cache lines.
+//                       slot word: bits  0..15 placement (0..P-1 PM, P = WAIT,
+//                                             P+1 = NULL)
+//                                  bits 16..23 vm_cpu in hundredths (np.around
+//                                             (.,2) makes every size k/100
+//                                             exactly, env.py:212-219)
+//                                  bits 24..31 vm_memory in hundredths
+//                       time word: waiting VM: remaining runtime (env.py:290);
+//                                  running VM: finish key F = timestep +
+//                                  remaining, so a running VM's words do not
+//                                  change while it runs (the step kernels
+//                                  store only the words that changed)
 //   pm   f64 [N][2][P] cpu[P] then memory[P]; kept in f64 because their values
 //                       carry the reference's accumulated rounding history
 //   hdr  EnvHdr [N]    256 B: 4 PCG64 streams, sequence bases, counters, stats
@@ -35,6 +41,12 @@ constexpr int kEnvWavesPerBlock = VMP_ENV_WPB;
 constexpr int kMaxVPT = 16;  // VM slots per lane held in registers: V <= 1024
 constexpr int kMaxStepsPerLaunch = 256;  // rollout launches are split by the host
 constexpr int kSpecDraws = 64;           // speculative service draws per launch
+
+// VM words (see vmw above): u32 elements per env, and the slot / time word of
+// slot v inside an env's block array
+__host__ __device__ inline int64_t vm_pitch(int V) { return (int64_t)((V + 63) >> 6) << 7; }
+__host__ __device__ inline int vm_slot_idx(int v) { return ((v >> 6) << 7) | (v & 63); }
+__host__ __device__ inline int vm_time_idx(int v) { return ((v >> 6) << 7) | 64 | (v & 63); }
 
 struct alignas(16) EnvHdr {
   uint64_t rng[4][4];      // [stream][state_hi, state_lo, inc_hi, inc_lo]; rng1..rng4
@@ -76,7 +88,7 @@ struct EnvParams {
   double beta, seq_lo, seq_range;
   const PoisConst *pois;  // device copy: [0] arrivals, [1] service lengths
   uint64_t *stamps;       // [N][8] phase clocks (diagnostic builds only)
-  uint64_t *vmw;
+  uint32_t *vmw;          // [N][vm_pitch(V)] (slot words | time words per 64-slot block)
   double *pm;
   EnvHdr *hdr;
   // per-wave LDS carve (bytes); offsets inside one wave's region

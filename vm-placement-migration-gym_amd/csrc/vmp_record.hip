@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void k_record(EnvParams p, RecArgs r) {
   uint32_t *hp = r.hist + (int64_t)e * 2 * kRecBins, *hs = hp + kRecBins;
   double life_sum = 0.0, life_cnt = 0.0, sc = 0.0, sm = 0.0;
   for (int v = lane; v < V; v += 64) {
-    const uint64_t w = p.vmw[base + v];
+    const uint32_t w = p.vmw[(int64_t)e * vm_pitch(V) + vm_slot_idx(v)];
     const int st = (int)(w & 0xFFFFu);
     const int pv = r.prev[base + v];
     const int a = r.act[base + v];
@@ -184,7 +184,7 @@ __global__ void k_record_init(EnvParams p, RecArgs r) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nv = (int64_t)p.N * p.V;
   if (i < nv) {
-    r.prev[i] = (uint16_t)(p.vmw[i] & 0xFFFFu);
+    r.prev[i] = (uint16_t)(p.vmw[(i / p.V) * vm_pitch(p.V) + vm_slot_idx((int)(i % p.V))] & 0xFFFFu);
     r.life_n[i] = 0;
     r.alloc[i] = -1;
     r.waits[i] = 0;
