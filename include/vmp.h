@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 8
+#define VMP_ABI_VERSION 9
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -294,12 +294,19 @@ int vmp_actor_head_bf16_fwd(int32_t B, int32_t K, int32_t V, int32_t A, const ui
  * with g_logprob / g_entropy f32[B] (nullable: 0), masked entries 0, as
  * vmp_policy_head_backward_bf16 computes from stored logits. The caller runs
  * it over row chunks (pointers offset to the chunk) and feeds each chunk's
- * dlogits to the dW / dh GEMMs, so no [B, V*A] tensor is ever allocated. */
+ * dlogits to the dW / dh GEMMs, so no [B, V*A] tensor is ever allocated.
+ * dbias (nullable): f32[V*A], ADDED to: the bias gradient of the chunk, the
+ * column sums of its dlogits in f32 before the bf16 rounding, formed inside
+ * the kernel (per-wave sums in LDS, one partial per M group, reduced in a
+ * fixed order: run-to-run identical), so no pass over the dlogits computes
+ * it. workspace (nullable): vmp_actor_head_bf16_bwd_workspace(B, V, A) floats
+ * for the partials (else stream-ordered memory is allocated). */
 int vmp_actor_head_bf16_bwd(int32_t B, int32_t K, int32_t V, int32_t A, const uint16_t *h,
                             const uint16_t *weight, const float *bias, const uint32_t *mask_bits,
                             const int32_t *action, const float *g_logprob,
-                            const float *g_entropy, uint16_t *dlogits, int32_t ld,
-                            void *hip_stream);
+                            const float *g_entropy, uint16_t *dlogits, int32_t ld, float *dbias,
+                            float *workspace, void *hip_stream);
+int64_t vmp_actor_head_bf16_bwd_workspace(int32_t B, int32_t V, int32_t A);
 
 /* Eval-mode Record metrics on the device (record.py:34-134, base.py:131-148):
  * on = 1 allocates the recorder and starts it from the current state (call it

@@ -4,11 +4,13 @@ vmp_actor_head_bf16_fwd/_bwd (BF16FusedActorHead) against the logits path of
 the same bf16 leg (BF16ActorHead: hipBLASLt bf16 GEMM with f32 logits + the
 tiled HIP head) and a plain-PyTorch fp32 head on the same bf16-rounded
 operands. Tolerances: logprob / entropy 1e-5 relative (f32 accumulation of
-the same bf16 products in another order); parameter gradients 1e-3 relative
-L2 against the logits path (both paths round dlogits to bf16 before the
-dW / dh GEMMs) and 1e-2 relative L2 against torch fp32 autograd of a
-plain-PyTorch head on the bf16-rounded operands (no HIP code on that side:
-the fused path's only extra rounding is its bf16 dlogits). Memory: a
+the same bf16 products in another order); x / W gradients 1e-3 relative L2
+against the logits path (both paths round dlogits to bf16 before the dW / dh
+GEMMs) and 1e-2 against torch fp32 autograd of a plain-PyTorch head on the
+bf16-rounded operands (no HIP code on that side: the fused path's only extra
+rounding is its bf16 dlogits); the bias gradient, summed in f32 inside the
+backward kernel from unrounded dlogits, 1e-4 against fp32 autograd (and 1e-2
+against the logits path, which sums bf16-rounded dlogits). Memory: a
 bf16 update on the fused path stays below one minibatch's f32 [B, V*A]
 logits; the logits path does not."""
 import numpy as np
@@ -105,15 +107,20 @@ def test_fused_matches_logits_path_and_torch(B, K, V, A):
     glp0[0] = 0.0
     lp_f, _, gx_f, gw_f, gb_f = _run(True, h, w, b, bits, act, V, A, glp0, gen, chunk_rows=512)
     _, _, gx_u, gw_u, gb_u = _run(False, h, w, b, bits, act, V, A, glp0, gen)
-    for name, f, u in (("x", gx_f, gx_u), ("w", gw_f, gw_u), ("b", gb_f, gb_u)):
+    # the logits path sums bf16-rounded dlogits for db; the fused kernel sums
+    # them in f32 before the rounding (closer to fp32, checked below)
+    for name, f, u, tol in (("x", gx_f, gx_u, 1e-3), ("w", gw_f, gw_u, 1e-3),
+                            ("b", gb_f, gb_u, 1e-2)):
         assert torch.isfinite(f).all(), name
-        assert _rel(f, u) < 1e-3, (name, _rel(f, u))
+        assert _rel(f, u) < tol, (name, _rel(f, u))
     # independent of every HIP path: torch fp32 autograd through a plain-PyTorch
-    # head on the bf16-rounded operands (the fused path rounds dlogits to bf16
-    # before its dW / dh GEMMs: 1e-2 relative L2 allowed, ~2e-3 expected)
+    # head on the bf16-rounded operands. x / W: the fused path rounds dlogits to
+    # bf16 before its dW / dh GEMMs (1e-2 relative L2 allowed, ~2e-3 expected);
+    # b: f32 column sums of unrounded dlogits inside the kernel (1e-4)
     gx_r, gw_r, gb_r = _torch_fp32_grads(h, w, b, bits, act, V, A, glp0, gen)
-    for name, f, r in (("x", gx_f, gx_r), ("w", gw_f, gw_r), ("b", gb_f, gb_r)):
-        assert _rel(f, r) < 1e-2, (name, "vs fp32 autograd", _rel(f, r))
+    for name, f, r, tol in (("x", gx_f, gx_r, 1e-2), ("w", gw_f, gw_r, 1e-2),
+                            ("b", gb_f, gb_r, 1e-4)):
+        assert _rel(f, r) < tol, (name, "vs fp32 autograd", _rel(f, r))
     # chunking does not change the result: one chunk == many chunks (same sums per chunk row)
     _, _, gx_1, gw_1, gb_1 = _run(True, h, w, b, bits, act, V, A, glp0, gen, chunk_rows=1 << 20)
     assert _rel(gx_1, gx_f) < 1e-6 and _rel(gw_1, gw_f) < 1e-6 and _rel(gb_1, gb_f) < 1e-6

@@ -90,9 +90,18 @@ def main():
         dl = torch.empty((r, N), dtype=torch.bfloat16, device=dev)
         tb = timeit(lambda: H.actor_head_bf16_bwd(hb[:r], wb, b, V, A, bits[:r], act[:r], glp[:r],
                                                   gen[:r], dl), n=10)
+        db = torch.zeros((N,), dtype=torch.float32, device=dev)
+        ws = torch.empty((H.bf16_bwd_workspace(r, V, A),), dtype=torch.float32, device=dev)
+        tbd = timeit(lambda: H.actor_head_bf16_bwd(hb[:r], wb, b, V, A, bits[:r], act[:r],
+                                                   glp[:r], gen[:r], dl, dbias=db, workspace=ws),
+                     n=10)
+        ones = torch.ones((1, r), dtype=torch.bfloat16, device=dev)
+        tg = timeit(lambda: torch.mm(ones, dl, out_dtype=torch.float32), n=10)
         print(json.dumps({"lib": os.environ.get("VMP_LIB_PATH", "default").split("/")[-1],
                           "fused_fwd_ms": t, "fused_fwd_tflops": flop / t / 1e9,
                           "bwd_ms_per_204800": tb * B / r,
+                          "bwd_with_dbias_ms_per_204800": tbd * B / r,
+                          "db_gemv_ms_per_204800": tg * B / r,
                           "bwd_tflops": 2.0 * r * K * N / tb / 1e9}), flush=True)
         return
     # hipBLASLt on the same GEMM: f32 logits out (what the logits path writes), bf16 out

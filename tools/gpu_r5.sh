@@ -26,6 +26,7 @@ for s in "$@"; do
     ppo16s) timeout -k 10 300 python tools/bench_ppo.py --precision bf16 --envs 8192 --updates 3 --warmup 1 --lookahead 0 > $O/ppo_bf16_sync.log 2>&1; rc=$?
            tail -1 $O/ppo_bf16_sync.log | cut -c1-800 ;;
     dwaug) timeout -k 10 120 python tools/bench_dw_aug.py > $O/dwaug.log 2>&1; rc=$?; tail -1 $O/dwaug.log ;;
+    hgbench) FWD_ONLY=1 timeout -k 10 300 python tools/bench_actor_head_bf16.py > $O/hgbench.log 2>&1; rc=$?; tail -1 $O/hgbench.log ;;
     counters) timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1; rc=$? ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac

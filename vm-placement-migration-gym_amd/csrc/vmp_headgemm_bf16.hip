@@ -75,6 +75,7 @@ struct H16Args {
   const float *g_lp, *g_ent;
   float *row_lp, *row_ent;  // forward: per (sample, VM row)
   uint16_t *dl;             // backward: bf16 dlogits [B][ld]
+  float *dpart;             // backward, nullable: bias-gradient partials [M group][V*A]
 };
 
 __device__ __forceinline__ int lds_chunk(int row, int cl) { return cl ^ ((row >> 1) & 7); }
@@ -194,10 +195,23 @@ __device__ __forceinline__ bool hg16_tile(const H16Args &a, int &n_tile, int &g)
 }
 
 // The epilogue of one M block: per sample column mc, per segment s, in registers.
+// Sum over the 16 lanes of a DPP row (lane 16 q + c, c = 0..15: the 16
+// samples of one q group) by inclusive row_shr prefix adds: lane c = 15 ends
+// with the row's total (a fixed order: run-to-run identical).
+__device__ __forceinline__ float row16_total(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xF, 0xF, false));
+  return x;
+}
+
+// colL (backward with a.dpart, else null): the wave's f32 column sums of
+// dlogits over every sample it has processed, one float per tile column.
 template <int TS, bool BWD, int NW>
 __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
                                               f32x4 (&acc)[kMaxNT / TS * TS][16 / NW], int m0,
-                                              int v0, int wid, int lane) {
+                                              int v0, int wid, int lane, float LDSP *colL) {
   constexpr int S = kMaxNT / TS, MC = 16 / NW;
   constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
   const int q = lane >> 4, c = lane & 15;
@@ -313,6 +327,18 @@ __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
             dd += (16 * u + r == tq) ? glp : 0.f;
             d[r] = ((u < TS - 1 || j < a.A) && !((nib[u] >> r) & 1u)) ? dd : 0.f;  // inner tiles: j < A
           }
+          if (colL) {
+            // the bias gradient db = 1^T dlogits (ppo.py:258-287 through the
+            // last Linear's bias): this row group's f32 column sums before the
+            // bf16 rounding, added to the wave's LDS sums by lane c = 15
+            float cs[4];
+#pragma unroll
+            for (int r = 0; r < 4; r++) cs[r] = row16_total(live ? d[r] : 0.f);
+            if (c == 15) {
+#pragma unroll
+              for (int r = 0; r < 4; r++) colL[16 * (s * TS + u) + 4 * q + r] += cs[r];
+            }
+          }
           // bf16 dlogits (round to nearest even), columns v A + j of row m
           const int j0 = 16 * u + 4 * q;
           const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
@@ -345,6 +371,33 @@ __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
   }
 }
 
+// The workgroup's bias-gradient partial: its waves' LDS column sums added in
+// wave order and stored to a.dpart[g][v A + j] (one workgroup per (column
+// tile, M group) pair, so every partial is written exactly once; k_dsum
+// reduces the M groups in order).
+template <int TS, int NW>
+__device__ __forceinline__ void hg16_dsum_flush(const H16Args &a, const float LDSP *cols, int v0,
+                                                int g) {
+  constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
+  __syncthreads();
+  for (int n = threadIdx.x; n < BNp; n += 64 * NW) {
+    const int s = n / SA, j = n - s * SA, v = v0 + s;
+    float x = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; w++) x += cols[w * BNp + n];
+    if (v < a.V && j < a.A) a.dpart[(int64_t)g * a.V * a.A + v * a.A + j] = x;
+  }
+}
+
+// db[n] += sum over the M groups g < G of part[g][n], in g order
+__global__ void k_dsum(int64_t N, int G, const float *part, float *db) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float x = 0.f;
+  for (int g = 0; g < G; g++) x += part[(int64_t)g * N + n];
+  db[n] += x;
+}
+
 // NW waves per workgroup, each owning MC = 16 / NW columns of 16 samples
 // (built: 8 waves x 2 columns, two waves per SIMD). Two LDS stages of BK = 64.
 template <int TS, bool BWD, int NW>
@@ -360,12 +413,16 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   int n_tile, g;
   if (!hg16_tile(a, n_tile, g)) return;
   const int v0 = n_tile * S;
+  const bool dsum = BWD && a.dpart;  // backward: the bias gradient's column sums too
+  float LDSP *colL = dsum ? biasL + BNp + wid * BNp : nullptr;
 
   // the tile's bias in tile-column order (0 past A / past V)
   for (int n = t; n < BNp; n += kThreads) {
     const int s = n / SA, j = n - s * SA, v = v0 + s;
     biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
   }
+  if (dsum)
+    for (int n = t; n < NW * BNp; n += kThreads) biasL[BNp + n] = 0.f;
   __syncthreads();
 
   const int nk = a.K / kBK;
@@ -435,8 +492,9 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
       for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
     continue;
 #endif
-    hg16_epilogue<TS, BWD, NW>(a, acc, m0, v0, wid, lane);
+    hg16_epilogue<TS, BWD, NW>(a, acc, m0, v0, wid, lane, colL);
   }
+  if (dsum) hg16_dsum_flush<TS, NW>(a, biasL + BNp, v0, g);
 }
 
 // ---- the deep-pipeline kernel: BK = 32 (64-B rows), NS LDS stages ----
@@ -499,10 +557,14 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16d(H16Args a) {
   int n_tile, g;
   if (!hg16_tile(a, n_tile, g)) return;
   const int v0 = n_tile * S;
+  const bool dsum = BWD && a.dpart;
+  float LDSP *colL = dsum ? biasL + BNp + wid * BNp : nullptr;
   for (int n = t; n < BNp; n += kThreads) {
     const int s = n / SA, j = n - s * SA, v = v0 + s;
     biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
   }
+  if (dsum)
+    for (int n = t; n < NW * BNp; n += kThreads) biasL[BNp + n] = 0.f;
   const int nk = a.K / kBK2;
   const int nblk = (a.m_blocks - g + a.m_groups - 1) / a.m_groups;
   const int total = nblk * nk;
@@ -565,7 +627,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16d(H16Args a) {
 #pragma unroll
         for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
 #else
-      hg16_epilogue<TS, BWD, NW>(a, acc, (g + bi * a.m_groups) * kBM, v0, wid, lane);
+      hg16_epilogue<TS, BWD, NW>(a, acc, (g + bi * a.m_groups) * kBM, v0, wid, lane, colL);
 #endif
 #pragma unroll
       for (int nt = 0; nt < NT; nt++) {
@@ -575,16 +637,19 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16d(H16Args a) {
       }
     }
   }
+  if (dsum) hg16_dsum_flush<TS, NW>(a, biasL + BNp, v0, g);
 }
 
+// stages, the tile's bias, the 8 waves' bias-gradient column sums (backward)
 template <int TS>
 constexpr size_t lds_bytes() {
-  return 2 * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow + 16 * (kMaxNT / TS * TS) * sizeof(float);
+  return 2 * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
 }
 template <int TS, int NS>
 constexpr size_t lds_bytes_deep() {
-  return NS * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow2 + 16 * (kMaxNT / TS * TS) * sizeof(float);
+  return NS * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow2 + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
 }
+static_assert(lds_bytes<1>() <= 160 * 1024, "stages exceed LDS");
 #ifndef VMP_HG16_NS
 #define VMP_HG16_NS 4  // deep kernel's LDS stages
 #endif
@@ -735,7 +800,7 @@ extern "C" int vmp_actor_head_bf16_bwd(int32_t B, int32_t K, int32_t V, int32_t 
                                        const float *bias, const uint32_t *mask_bits,
                                        const int32_t *action, const float *g_logprob,
                                        const float *g_entropy, uint16_t *dlogits, int32_t ld,
-                                       void *stream) {
+                                       float *dbias, float *workspace, void *stream) {
   int rc = check_common(B, K, V, A, h, weight, bias, mask_bits, action,
                         "vmp_actor_head_bf16_bwd: bad shape or null pointer");
   if (rc) return rc;
@@ -749,7 +814,38 @@ extern "C" int vmp_actor_head_bf16_bwd(int32_t B, int32_t K, int32_t V, int32_t 
   a.B = B, a.K = K, a.V = V, a.A = A, a.W32 = (A + 31) / 32, a.ld = ld;
   a.h = h, a.w = weight, a.bias = bias, a.bits = mask_bits, a.action = action;
   a.g_lp = g_logprob, a.g_ent = g_entropy, a.dl = dlogits;
-  hipError_t e = launch_hg16<true>(a, (hipStream_t)stream);
+  hipStream_t st = (hipStream_t)stream;
+  float *scratch = nullptr;
+  if (dbias) {  // partials per M group (at most bf16_bwd_workspace_floats floats)
+    a.dpart = workspace;
+    if (!a.dpart) {
+      hipError_t e = hipMallocAsync((void **)&scratch,
+                                    sizeof(float) * (size_t)vmp_actor_head_bf16_bwd_workspace(B, V, A),
+                                    st);
+      if (e != hipSuccess) return policy_fail(VMP_EOOM, hipGetErrorString(e));
+      a.dpart = scratch;
+    }
+  }
+  hipError_t e = launch_hg16<true>(a, st);
+  if (e == hipSuccess && dbias) {
+    const int64_t N = (int64_t)V * A;
+    const int G = a.m_groups < a.m_blocks ? a.m_groups : a.m_blocks;
+    hipLaunchKernelGGL(k_dsum, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, N, G, a.dpart,
+                       dbias);
+    e = hipGetLastError();
+  }
+  if (scratch) {
+    hipError_t f = hipFreeAsync(scratch, st);
+    if (e == hipSuccess) e = f;
+  }
   if (e != hipSuccess) return policy_fail(VMP_EDEVICE, hipGetErrorString(e));
   return VMP_OK;
+}
+
+// floats of bias-gradient partials vmp_actor_head_bf16_bwd may use: V*A per M
+// group, at most 64 groups x 8 (XCD teams) of 256-sample blocks
+extern "C" int64_t vmp_actor_head_bf16_bwd_workspace(int32_t B, int32_t V, int32_t A) {
+  const int64_t blocks = ((int64_t)B + kBM - 1) / kBM;
+  const int64_t groups = blocks < 512 ? blocks : 512;
+  return (groups < 1 ? 1 : groups) * (int64_t)V * A;
 }

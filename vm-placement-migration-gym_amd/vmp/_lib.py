@@ -18,7 +18,8 @@ EXPORTS = (
     "vmp_heuristic_step", "vmp_rollout_heuristic", "vmp_mask", "vmp_mask_bool", "vmp_get_obs",
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
     "vmp_policy_head", "vmp_policy_head_backward", "vmp_policy_head_backward_bf16",
-    "vmp_actor_head", "vmp_actor_head_bf16_fwd", "vmp_actor_head_bf16_bwd", "vmp_record_enable",
+    "vmp_actor_head", "vmp_actor_head_bf16_fwd", "vmp_actor_head_bf16_bwd",
+    "vmp_actor_head_bf16_bwd_workspace", "vmp_record_enable",
     "vmp_record_read", "vmp_snapshot_bytes", "vmp_snapshot", "vmp_restore",
     "vmp_debug_fail_alloc", "vmp_debug_live_allocs", "vmp_debug_stamps", "vmp_debug_occupancy",
     "vmp_debug_quiet_violations",
@@ -96,7 +97,8 @@ def lib():
                                            P, P, P, P, P, P, P]),
         "vmp_actor_head_bf16_fwd": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, P, P, P, P, P]),
         "vmp_actor_head_bf16_bwd": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, P, P, P, P,
-                                                    i32, P]),
+                                                    i32, P, P, P]),
+        "vmp_actor_head_bf16_bwd_workspace": (ctypes.c_int64, [i32, i32, i32]),
         "vmp_record_enable": (ctypes.c_int, [P, i32]),
         "vmp_record_read": (ctypes.c_int, [P, P, P]),
         "vmp_snapshot_bytes": (ctypes.c_int, [P, P]),
@@ -115,7 +117,7 @@ def lib():
         if f is None:
             raise VmpError(f"libvmp lacks {name}")
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 8:
+    if L.vmp_abi_version() != 9:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

@@ -281,10 +281,13 @@ def actor_head_bf16_fwd(hb, wb, bias, V, A, bits, action):
     return act, lp, ent
 
 
-def actor_head_bf16_bwd(hb, wb, bias, V, A, bits, action, g_lp, g_ent, out):
+def actor_head_bf16_bwd(hb, wb, bias, V, A, bits, action, g_lp, g_ent, out, dbias=None,
+                        workspace=None):
     """The bf16 training backward (vmp_actor_head_bf16_bwd) over the rows of hb
     (a chunk): recomputes the logits tiles and writes bf16 dlogits into `out`
-    ([rows, >= V*A], row stride out.stride(0))."""
+    ([rows, >= V*A], row stride out.stride(0)); with `dbias` (f32 [V*A]) the
+    chunk's bias gradient is ADDED to it from inside the kernel (workspace:
+    f32 of bf16_bwd_workspace(rows, V, A) elements, optional)."""
     B, K, act = _bf16_operands(hb, wb, bias, V, A, bits, action, "actor_head_bf16_bwd")
     if (out.dtype != torch.bfloat16 or out.dim() != 2 or out.shape[0] < B
             or out.shape[1] < V * A or out.stride(1) != 1):
@@ -293,10 +296,22 @@ def actor_head_bf16_bwd(hb, wb, bias, V, A, bits, action, g_lp, g_ent, out):
         raise ValueError("dlogits out must be 4-byte aligned")
     glp = None if g_lp is None else g_lp.float().contiguous()
     gen = None if g_ent is None else g_ent.float().contiguous()
+    if dbias is not None and (dbias.dtype != torch.float32 or dbias.numel() != V * A
+                              or not dbias.is_contiguous()):
+        raise ValueError("dbias must be contiguous f32 [V*A]")
+    if workspace is not None and (workspace.dtype != torch.float32
+                                  or workspace.numel() < bf16_bwd_workspace(B, V, A)):
+        raise ValueError("workspace must be f32 with bf16_bwd_workspace(B, V, A) elements")
     check(lib().vmp_actor_head_bf16_bwd(B, K, V, A, ptr(hb), ptr(wb), ptr(bias.contiguous()),
                                         ptr(bits), ptr(act), ptr(glp), ptr(gen), ptr(out),
-                                        int(out.stride(0)), _stream(hb)))
+                                        int(out.stride(0)), ptr(dbias), ptr(workspace),
+                                        _stream(hb)))
     return out
+
+
+def bf16_bwd_workspace(B, V, A):
+    """f32 elements of vmp_actor_head_bf16_bwd's bias-gradient partials."""
+    return int(lib().vmp_actor_head_bf16_bwd_workspace(int(B), int(V), int(A)))
 
 
 def det_action(logits, V, A):

@@ -210,26 +210,27 @@ class BF16FusedActorHead(torch.autograd.Function):
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         dl = torch.empty((R, N), dtype=torch.bfloat16, device=dev)
         gx = torch.empty((B, K), dtype=torch.float32, device=dev) if need_x else None
-        # dW = dlogits^T h and db = 1^T dlogits, per chunk. (The
-        # bias column appended to h, dlogits^T [h | 1 | 0...], falls off
-        # hipBLASLt's fast kernels: 3.7 ms vs 2.4 + 0.8 ms per 70 144-row chunk,
-        # profiles/r04_hg16_gemm_layouts.log.)
-        gw = gb = None
-        ones = torch.ones((1, R), dtype=torch.bfloat16, device=dev) if need_b else None
+        # dW = dlogits^T h per chunk (hipBLASLt); db = 1^T dlogits is summed by
+        # the backward kernel itself (f32 column sums before the bf16
+        # rounding, reduced per M group in a fixed order), so no pass over the
+        # dlogits and no second stream computes it (round 4 ran a 1^T d GEMV,
+        # 0.87 ms per 70 144-row chunk; d^T [h | 1 | 0...] at K + 64 columns
+        # costs as much, profiles/r05_dw_aug.log)
+        gw = None
+        gb = torch.zeros((N,), dtype=torch.float32, device=dev) if need_b else None
+        ws = (torch.empty((H.bf16_bwd_workspace(R, V, A),), dtype=torch.float32, device=dev)
+              if need_b else None)
         for r0 in range(0, B, R):
             r1 = min(B, r0 + R)
             n = r1 - r0
             d = dl[:n]
             H.actor_head_bf16_bwd(xb[r0:r1], wb, b, V, A, None if bits is None else bits[r0:r1],
-                                  act[r0:r1], glp[r0:r1], gen[r0:r1], d)
+                                  act[r0:r1], glp[r0:r1], gen[r0:r1], d, dbias=gb, workspace=ws)
             if need_x:
                 gx[r0:r1] = torch.mm(d, wb, out_dtype=torch.float32)
             if need_w:
                 part = torch.mm(d.t(), xb[r0:r1], out_dtype=torch.float32)
                 gw = part if gw is None else gw.add_(part)
-            if need_b:  # (d.sum(0, dtype=float32) would allocate an f32 copy of d)
-                part = torch.mm(ones[:, :n], d, out_dtype=torch.float32)[0]
-                gb = part if gb is None else gb.add_(part)
         return gx, gw, gb, None, None, None, None, None
 
 
