@@ -195,15 +195,27 @@ __device__ __forceinline__ bool hg16_tile(const H16Args &a, int &n_tile, int &g)
 }
 
 // The epilogue of one M block: per sample column mc, per segment s, in registers.
-// Sum over the 16 lanes of a DPP row (lane 16 q + c, c = 0..15: the 16
-// samples of one q group) by inclusive row_shr prefix adds: lane c = 15 ends
-// with the row's total (a fixed order: run-to-run identical).
-__device__ __forceinline__ float row16_total(float x) {
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xF, 0xF, false));
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xF, 0xF, false));
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xF, 0xF, false));
-  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xF, 0xF, false));
-  return x;
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+// Column sums of four values d[0..3] (columns 4 q + r of one tile, sample c =
+// lane & 15) over the 16 samples of a DPP row, reduce-scatter style: two
+// quad exchanges leave each lane one column summed over its quad, two
+// row_shr prefix adds sum the four quads; lane c = 12..15 returns the total
+// of column r = 2 (c & 1) + ((c >> 1) & 1). A fixed order: run-to-run
+// identical. 11 VALU per four columns.
+__device__ __forceinline__ float row16_colsum4(const float (&d)[4], int c) {
+  const bool odd = c & 1, b2 = (c >> 1) & 1;
+  float k0 = odd ? d[2] : d[0], k1 = odd ? d[3] : d[1];
+  const float s0 = odd ? d[0] : d[2], s1 = odd ? d[1] : d[3];
+  k0 += dpp_f<0xB1>(s0);  // quad_perm [1, 0, 3, 2]: the partner c ^ 1
+  k1 += dpp_f<0xB1>(s1);
+  float k = b2 ? k1 : k0;
+  k += dpp_f<0x4E>(b2 ? k0 : k1);  // quad_perm [2, 3, 0, 1]: the partner c ^ 2
+  k += dpp_f<0x114>(k);            // row_shr:4
+  k += dpp_f<0x118>(k);            // row_shr:8
+  return k;
 }
 
 // colL (backward with a.dpart, else null): the wave's f32 column sums of
@@ -331,13 +343,11 @@ __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
             // the bias gradient db = 1^T dlogits (ppo.py:258-287 through the
             // last Linear's bias): this row group's f32 column sums before the
             // bf16 rounding, added to the wave's LDS sums by lane c = 15
-            float cs[4];
+            float dl4[4];
 #pragma unroll
-            for (int r = 0; r < 4; r++) cs[r] = row16_total(live ? d[r] : 0.f);
-            if (c == 15) {
-#pragma unroll
-              for (int r = 0; r < 4; r++) colL[16 * (s * TS + u) + 4 * q + r] += cs[r];
-            }
+            for (int r = 0; r < 4; r++) dl4[r] = live ? d[r] : 0.f;
+            const float cs = row16_colsum4(dl4, c);
+            if (c >= 12) colL[16 * (s * TS + u) + 4 * q + 2 * (c & 1) + ((c >> 1) & 1)] += cs;
           }
           // bf16 dlogits (round to nearest even), columns v A + j of row m
           const int j0 = 16 * u + 4 * q;
