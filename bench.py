@@ -343,11 +343,14 @@ def issue_roofline(pmc, N, kern_ms):
     cyc_prof = clk * float(pmc["avg_ns"]) * 1e-9
     valu, salu = float(pmc["SQ_INSTS_VALU"]), float(pmc.get("SQ_INSTS_SALU", 0.0))
     lds = float(pmc.get("SQ_INSTS_LDS", 0.0))
+    busy = pmc.get("valu_busy")  # rocprofv3's VALUBusy of the same pass, if collected
     return {"bound": "valu-issue", "unit": "SIMD issue cycles",
             "valu_insts_per_env_step": valu / N, "salu_insts_per_env_step": salu / N,
             "lds_insts_per_env_step": lds / N,
             "frac": 2.0 * valu / (N_SIMDS * cyc),
             "frac_at_profile_time": 2.0 * valu / (N_SIMDS * cyc_prof),
+            "valu_busy_pmc": busy,
+            "valu_busy_pmc_at_live_time": None if busy is None else busy * cyc_prof / cyc,
             "valu_frac_single_wave": 4.0 * valu / (N_SIMDS * cyc),
             "clock_GHz": clk / 1e9, "profile_kernel_ms": float(pmc["avg_ns"]) * 1e-6,
             "source": "profiles/traffic.json (rocprofv3 --pmc SQ_INSTS_VALU/SALU/LDS, "

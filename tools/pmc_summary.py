@@ -35,6 +35,11 @@ if "GRBM_GUI_ACTIVE" in avg:
     out["eff_clock_GHz"] = avg["GRBM_GUI_ACTIVE"] / 8 / dur
 if "SQ_WAVE_CYCLES" in avg and "SQ_BUSY_CYCLES" in avg:
     out["avg_waves_resident"] = avg["SQ_WAVE_CYCLES"] / avg["SQ_BUSY_CYCLES"]
+if "SQ_ACTIVE_INST_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+    # rocprofv3's derived VALUBusy: 100 * SQ_ACTIVE_INST_VALU / CU_NUM / GRBM_GUI_ACTIVE
+    # (per-XCD GRBM: the summed counter / 8); SQ_ACTIVE_INST_VALU is in quad-cycles
+    # per SIMD, so x4 cycles / 4 SIMDs per CU cancel
+    out["valu_busy"] = avg["SQ_ACTIVE_INST_VALU"] / 256 / (avg["GRBM_GUI_ACTIVE"] / 8)
 if "FETCH_SIZE" in avg:
     out["hbm_read_bytes_corrected"] = 2 * avg["FETCH_SIZE"] * 1024
 if "WRITE_SIZE" in avg:

@@ -30,7 +30,7 @@ def kclass(name):
         return "head forward (HIP)"
     if "k_head_bwd" in name:
         return "head backward (HIP)"
-    if "k_hg16" in name:
+    if "k_hg16" in name or "k_dsum" in name:
         return "fused bf16 GEMM + head, training (HIP)"
     if "k_head_gemm" in name or "k_hg_" in name:
         return "fused GEMM + head (HIP)"
