@@ -27,6 +27,8 @@ for s in "$@"; do
            tail -1 $O/ppo_bf16_sync.log | cut -c1-800 ;;
     dwaug) timeout -k 10 120 python tools/bench_dw_aug.py > $O/dwaug.log 2>&1; rc=$?; tail -1 $O/dwaug.log ;;
     hgbench) FWD_ONLY=1 timeout -k 10 300 python tools/bench_actor_head_bf16.py > $O/hgbench.log 2>&1; rc=$?; tail -1 $O/hgbench.log ;;
+    timeline) timeout -k 10 300 python tools/update_timeline.py > $O/timeline.log 2>&1; rc=$?; tail -c 600 $O/timeline.log ;;
+    hostprof) timeout -k 10 300 python tools/host_prof_values.py > $O/hostprof.log 2>&1; rc=$?; grep -E "get_value|tottime" $O/hostprof.log ;;
     counters) timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1; rc=$? ;;
     *) echo "unknown step $s"; rc=2 ;;
   esac

@@ -252,11 +252,19 @@ def _host_scalar(t):
     return read
 
 
+BF16_MIN_OUT = 16  # narrower Linears (the critic's value head) stay f32
+
+
 def _run_mlp(seq, x, precision):
+    """seq(x); in bf16 precision every Linear of >= BF16_MIN_OUT outputs runs as
+    BF16Linear. The critic's 512 -> 1 value head stays an f32 Linear: its
+    GEMV is a bandwidth-bound 2 KB-per-row read, and hipBLASLt's bf16 -> f32
+    addmm at N = 1 costs ~17 ms of host time per call on ROCm 7 / torch 2.10
+    (tools/host_prof_values.py), which serialised the update's value pass."""
     if precision != "bf16":
         return seq(x)
     for m in seq:
-        if isinstance(m, nn.Linear):
+        if isinstance(m, nn.Linear) and m.out_features >= BF16_MIN_OUT:
             x = BF16Linear.apply(x, m.weight, m.bias)
         else:
             x = m(x)
