@@ -60,6 +60,12 @@ int64_t quiet_violations_take() {
 #endif
 }
 
+// Register row s of lane ln (slot v = 64 s + ln) in the blocked VM words of
+// a wave kernel: the slot word's index (= vm_slot_idx(v)), + 64 for the time
+// word. vm_pitch pads the env's blocks to the kernel's rows, so a padded slot
+// (v >= V) reads padding inside the env's pitch, never used.
+__device__ __forceinline__ int vw_row(int s, int ln) { return (s << 7) + ln; }
+
 // Streaming stores (obs / state written once per launch, not re-read by it).
 #ifdef VMP_NT_STORE
 #define ST_NT(ptr, val) __builtin_nontemporal_store((val), gptr(ptr))
@@ -1883,12 +1889,12 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
 #pragma unroll
   for (int s = 0; s < VPT; s++) {
     const int v = s * 64 + lane;
-    const uint32_t x = vlo[vm_slot_idx(min(v, V - 1))];
+    const uint32_t x = vlo[vw_row(s, lane)];
     wa[s] = v < V ? x : (uint32_t)kPad;
     if (ONE) {
       rem[s] = 0;
     } else {
-      const uint32_t y = vlo[vm_time_idx(min(v, V - 1))];
+      const uint32_t y = vlo[vw_row(s, lane) + 64];
       rem[s] = v < V ? y : 0u;
     }
   }
@@ -1950,7 +1956,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   if (ONE && !EXT) {
     // issued before the action phase, consumed after it (latency hidden by it)
 #pragma unroll
-    for (int s = 0; s < VPT; s++) hiv[s] = vlo[vm_time_idx(min(s * 64 + lane, V - 1))];
+    for (int s = 0; s < VPT; s++) hiv[s] = vlo[vw_row(s, lane) + 64];
     __asm__ volatile("" ::: "memory");
   }
   uint32_t *vmo = p.vmw + (int64_t)e * vm_pitch(V);
@@ -1979,7 +1985,7 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
       if (ONE) {
         const int ln = fresh_lane();
 #pragma unroll
-        for (int s = 0; s < VPT; s++) hiv[s] = vlo[vm_time_idx(min(s * 64 + ln, V - 1))];
+        for (int s = 0; s < VPT; s++) hiv[s] = vlo[vw_row(s, ln) + 64];
       }
     }
     STAMP(1);
@@ -2041,16 +2047,17 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     for (int s = 0; s < VPT; s++) {
       const int v = s * 64 + ln;
       if (live(wa[s]) && ((dirty >> s) & 1u)) {  // unchanged words stay as they are
+        const int iw = (s << 7) + ln;  // live: v < V, so vm_slot_idx(v)
         if (!ONE) {
-          ST_NT(vmo + vm_slot_idx(v), wa[s]);
-          ST_NT(vmo + vm_time_idx(v), rem[s]);
+          ST_NT(vmo + iw, wa[s]);
+          ST_NT(vmo + iw + 64, rem[s]);
         } else if (w_pl(wa[s]) == P + 1) {  // finished: NULL, remaining 0
-          ST_NT(vmo + vm_slot_idx(v), wa[s]);
-          ST_NT(vmo + vm_time_idx(v), 0u);
+          ST_NT(vmo + iw, wa[s]);
+          ST_NT(vmo + iw + 64, 0u);
         } else {  // placed (r -> F = t + r) or suspended (F -> r = F - t)
           uint32_t GLBP *w32 = gptr(vmo);
-          w32[vm_slot_idx(v)] = wa[s];
-          __hip_atomic_fetch_add(w32 + vm_time_idx(v), w_pl(wa[s]) < P ? t32 : 0u - t32,
+          w32[iw] = wa[s];
+          __hip_atomic_fetch_add(w32 + iw + 64, w_pl(wa[s]) < P ? t32 : 0u - t32,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }

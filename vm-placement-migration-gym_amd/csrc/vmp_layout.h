@@ -44,7 +44,18 @@ constexpr int kSpecDraws = 64;           // speculative service draws per launch
 
 // VM words (see vmw above): u32 elements per env, and the slot / time word of
 // slot v inside an env's block array
-__host__ __device__ inline int64_t vm_pitch(int V) { return (int64_t)((V + 63) >> 6) << 7; }
+// (V <= 1024, the wave kernels: the block count is rounded up to the kernel's
+// slot rows per lane, 1 / 2 / 4 / 8 / 16, so row s of every lane lies inside
+// the env's pitch and the loads need no clamp)
+__host__ __device__ inline int64_t vm_pitch(int V) {
+  int b = (V + 63) >> 6;
+  if (V <= 1024) {
+    int q = 1;
+    while (q < b) q <<= 1;
+    b = q;
+  }
+  return (int64_t)b << 7;
+}
 __host__ __device__ inline int vm_slot_idx(int v) { return ((v >> 6) << 7) | (v & 63); }
 __host__ __device__ inline int vm_time_idx(int v) { return ((v >> 6) << 7) | 64 | (v & 63); }
 
