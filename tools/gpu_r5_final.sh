@@ -12,7 +12,7 @@ rc=$?; echo "smoke_rc=$rc"; tail -1 $O/smoke.log; [ $rc -ne 0 ] && exit $rc
 STEPS=20 WARMUP=5 bash tools/gpu_profile.sh > $O/prof.log 2>&1
 rc=$?; echo "prof_rc=$rc"; [ $rc -ne 0 ] && { tail $O/prof.log; exit $rc; }
 python3 tools/pmc_summary.py gpurun_out/prof 32768 --write $O/traffic.json > /dev/null && cp $O/traffic.json profiles/traffic.json
-find gpurun_out/prof/kt -name "*kernel_stats.csv" -exec cp {} $O/headline_kernel_stats.csv ;
+find gpurun_out/prof/kt -name "*kernel_stats.csv" -exec cp {} $O/headline_kernel_stats.csv \;
 rm -rf gpurun_out/prof/kt gpurun_out/prof/p1 gpurun_out/prof/p2 gpurun_out/prof/p3
 timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2>&1
 rc=$?; echo "bench_rc=$rc"; [ $rc -ne 0 ] && exit $rc
