@@ -126,6 +126,68 @@ def test_fused_matches_logits_path_and_torch(B, K, V, A):
     assert _rel(gx_1, gx_f) < 1e-6 and _rel(gw_1, gw_f) < 1e-6 and _rel(gb_1, gb_f) < 1e-6
 
 
+@pytest.mark.parametrize("B,K,V,A", [(1500, 512, 300, 102), (700, 256, 13, 39),
+                                     (333, 64, 7, 22), (300, 128, 5, 128), (4096, 512, 30, 12)])
+def test_ping_pong_kernel_bit_exact(monkeypatch, B, K, V, A):
+    """VMP_HG16_PP=2 / 3 (two wave groups, epilogue beside the other group's
+    matrix loop; 2 / 3 LDS stages) against the two-stage kernel: the same MFMA chains, the same
+    epilogue code and the same per-wave bias-gradient sums in the same order,
+    so logprob, entropy, dlogits and db are bit-identical (ragged B: the last
+    half block is partial or empty)."""
+    from vmp import head as H
+    h, w, b, mask, act = _case(B, K, V, A, seed=3 * B + V)
+    bits = H.pack_mask(mask, V, A)
+    hb, wb = h.bfloat16(), w.bfloat16()
+    g = torch.Generator().manual_seed(11)
+    glp = torch.randn(B, generator=g).to(DEV)
+    gen = torch.randn(B, generator=g).to(DEV)
+    outs = []
+    for pp in ("0", "2", "3"):
+        monkeypatch.setenv("VMP_HG16_PP", pp)
+        _, lp, ent = H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act)
+        dl = torch.full((B, V * A), 7, dtype=torch.bfloat16, device=DEV)
+        db = torch.zeros((V * A,), dtype=torch.float32, device=DEV)
+        H.actor_head_bf16_bwd(hb, wb, b, V, A, bits, act, glp, gen, dl, dbias=db)
+        torch.cuda.synchronize()
+        outs.append((lp, ent, dl, db))
+    for o in outs[1:]:
+        for name, x, y in zip(("logprob", "entropy", "dlogits", "dbias"), outs[0], o):
+            assert torch.equal(torch.nan_to_num(x.float()), torch.nan_to_num(y.float())), name
+
+
+@pytest.mark.parametrize("B,K,V,A", [(1500, 512, 300, 102), (700, 256, 13, 39),
+                                     (333, 64, 7, 22), (300, 128, 5, 128), (4096, 512, 30, 12),
+                                     (2100, 512, 301, 101)])
+@pytest.mark.parametrize("rd", ["2", "4"])
+def test_resident_w_kernel_matches_two_stage(monkeypatch, B, K, V, A, rd):
+    """VMP_HG16_RES=1 (W slab resident in LDS, h straight into registers,
+    512-sample blocks) against the two-stage kernel: the same MFMA chain per
+    logit (K chunks in order) and the same epilogue, so logprob, entropy and
+    dlogits are bit-identical; the bias gradient sums the same f32 column
+    partials grouped by other blocks, so it agrees to f32 rounding (ragged B,
+    V not a multiple of the tile's segments, A = 128 and 101)."""
+    from vmp import head as H
+    h, w, b, mask, act = _case(B, K, V, A, seed=5 * B + V)
+    bits = H.pack_mask(mask, V, A)
+    hb, wb = h.bfloat16(), w.bfloat16()
+    g = torch.Generator().manual_seed(13)
+    glp = torch.randn(B, generator=g).to(DEV)
+    gen = torch.randn(B, generator=g).to(DEV)
+    monkeypatch.setenv("VMP_HG16_RD", rd)
+    outs = []
+    for res in ("0", "1"):
+        monkeypatch.setenv("VMP_HG16_RES", res)
+        _, lp, ent = H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act)
+        dl = torch.full((B, V * A), 7, dtype=torch.bfloat16, device=DEV)
+        db = torch.zeros((V * A,), dtype=torch.float32, device=DEV)
+        H.actor_head_bf16_bwd(hb, wb, b, V, A, bits, act, glp, gen, dl, dbias=db)
+        torch.cuda.synchronize()
+        outs.append((lp, ent, dl, db))
+    for name, x, y in zip(("logprob", "entropy", "dlogits"), outs[0][:3], outs[1][:3]):
+        assert torch.equal(torch.nan_to_num(x.float()), torch.nan_to_num(y.float())), name
+    torch.testing.assert_close(outs[1][3], outs[0][3], rtol=1e-5, atol=1e-6 * B)
+
+
 def test_no_mask_and_deterministic():
     """bits = None (masked=False in PPOConfig) and run-to-run identical outputs."""
     B, K, V, A = 777, 512, 300, 102

@@ -68,6 +68,7 @@ constexpr float kLog2e = 1.44269504088896341f;
 struct H16Args {
   int B, K, V, A, W32, n_tiles, m_blocks, m_groups, ld;
   int team, teams;  // XCD teams (launch_hg16); team 0: one column tile per block index
+  int stag;         // resident-W kernel: block-walk stagger (hg16r walk)
   const uint16_t *h, *w;
   const float *bias;
   const uint32_t *bits;
@@ -87,10 +88,23 @@ __device__ __forceinline__ bf16x8 frag(const char LDSP *base, int row, int cl) {
 // global -> LDS staging of one K stage: W rows (tile columns, segment-padded)
 // then h rows, 8 rows of 128 B per wave instruction; lane L writes LDS
 // position L % 8 of row L / 8 with the logical chunk that position holds.
-template <int TS, int NT, int NW>
+// One global_load_lds_dwordx4 in inline asm: the compiler does not see an
+// LDS DMA, so it inserts no vmcnt wait of its own for it (the ping-pong
+// kernel's register reuse made it wait for the whole stage before the first
+// MFMA). The caller counts these in its own s_waitcnt vmcnt. M0 (the wave's
+// LDS destination) is written here only; no other code of the kernels that
+// use it reads M0.
+__device__ __forceinline__ void glds16_asm(const void *src, char LDSP *dst) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
+               : "memory");
+}
+
+// NW issuing waves (wid < NW), BM h rows; ASM: glds16_asm instead of the builtin.
+template <int TS, int NT, int NW, int BM = kBM, bool ASM = false>
 __device__ __forceinline__ void stage_issue(const H16Args &a, char LDSP *buf, int v0, int m0,
                                             int k0, int wid, int lane) {
-  constexpr int SA = 16 * TS, BNp = 16 * NT, PW = BNp / 8, PIECES = (BNp + kBM) / 8;
+  constexpr int SA = 16 * TS, BNp = 16 * NT, PW = BNp / 8, PIECES = (BNp + BM) / 8;
   const int rl = lane >> 3, p = lane & 7;
 #pragma unroll
   for (int i0 = 0; i0 < PIECES; i0 += NW) {
@@ -110,7 +124,8 @@ __device__ __forceinline__ void stage_issue(const H16Args &a, char LDSP *buf, in
       }
       src += k0 + 8 * lds_chunk(r, p);
       char LDSP *dst = buf + (i < PW ? 0 : BNp * kRow) + (r - rl) * kRow;
-      __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)dst, 16, 0, 0);
+      if (ASM) glds16_asm(src, dst);
+      else __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)dst, 16, 0, 0);
     }
   }
 }
@@ -194,7 +209,6 @@ __device__ __forceinline__ bool hg16_tile(const H16Args &a, int &n_tile, int &g)
   return g < a.m_blocks;
 }
 
-// The epilogue of one M block: per sample column mc, per segment s, in registers.
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
@@ -218,40 +232,57 @@ __device__ __forceinline__ float row16_colsum4(const float (&d)[4], int c) {
   return k;
 }
 
+// The epilogue of one wave's samples (MC columns of 16) of an M block, one
+// (column mc, segment s) row at a time: begin() loads the per-sample
+// gradients and row 0's mask / action, row(pi) consumes row pi and prefetches
+// row pi + 1 (the ping-pong kernel spreads the rows over the other group's
+// K steps, so the state between rows is these few registers and acc).
 // colL (backward with a.dpart, else null): the wave's f32 column sums of
 // dlogits over every sample it has processed, one float per tile column.
-template <int TS, bool BWD, int NW>
-__device__ __forceinline__ void hg16_epilogue(const H16Args &a,
-                                              f32x4 (&acc)[kMaxNT / TS * TS][16 / NW], int m0,
-                                              int v0, int wid, int lane, float LDSP *colL) {
-  constexpr int S = kMaxNT / TS, MC = 16 / NW;
-  constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
-  const int q = lane >> 4, c = lane & 15;
-  // ---- epilogue: per sample column mc, per segment s, in registers ----
+template <int TS, bool BWD, int MC, int SEG = kMaxNT / TS>
+struct Hg16Epi {
+  static constexpr int S = SEG, NP = MC * S;  // S segments of TS tiles per column tile
+  static constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
   // The (mc, s) rows' mask words and actions are loaded one row ahead (and
   // the backward's per-sample gradients up front), so a row's compute runs
   // under the next row's loads: loaded where used, every row waited on two
   // dependent global round trips, and each wait also drained the previous
   // row's dlogits stores.
-  constexpr int NP = MC * S;
-  auto row_of = [&](int pi) -> int64_t {
-    const int m = m0 + 16 * (MC * wid + pi / S) + c;
-    return (int64_t)(m < a.B ? m : a.B - 1) * a.V + min(v0 + pi % S, a.V - 1);
-  };
   float glp_[MC], gen_[MC];
-#pragma unroll
-  for (int mc = 0; mc < MC; mc++) {
-    const int m = m0 + 16 * (MC * wid + mc) + c;
-    const int mm = m < a.B ? m : a.B - 1;
-    glp_[mc] = (BWD && a.g_lp) ? a.g_lp[mm] : 0.f;
-    gen_[mc] = (BWD && a.g_ent) ? a.g_ent[mm] : 0.f;
-  }
   uint32_t mwn[4];
   int actn;
-  load_mask_raw<W32>(a, row_of(0), mwn);
-  actn = a.action[row_of(0)];
+
+  __device__ __forceinline__ static int64_t row_of(const H16Args &a, int pi, int m0, int v0, int wid,
+                                                   int c) {
+    const int m = m0 + 16 * (MC * wid + pi / S) + c;
+    return (int64_t)(m < a.B ? m : a.B - 1) * a.V + min(v0 + pi % S, a.V - 1);
+  }
+
+  __device__ __forceinline__ void keep_live() {
 #pragma unroll
-  for (int pi = 0; pi < NP; pi++) {
+    for (int i = 0; i < 4; i++) asm volatile("" : "+v"(mwn[i]));
+    asm volatile("" : "+v"(actn));
+    if (BWD)
+#pragma unroll
+      for (int mc = 0; mc < MC; mc++) asm volatile("" : "+v"(glp_[mc]), "+v"(gen_[mc]));
+  }
+
+  __device__ __forceinline__ void begin(const H16Args &a, int m0, int v0, int wid, int lane) {
+    const int c = lane & 15;
+#pragma unroll
+    for (int mc = 0; mc < MC; mc++) {
+      const int m = m0 + 16 * (MC * wid + mc) + c;
+      const int mm = m < a.B ? m : a.B - 1;
+      glp_[mc] = (BWD && a.g_lp) ? a.g_lp[mm] : 0.f;
+      gen_[mc] = (BWD && a.g_ent) ? a.g_ent[mm] : 0.f;
+    }
+    load_mask_raw<W32>(a, row_of(a, 0, m0, v0, wid, c), mwn);
+    actn = a.action[row_of(a, 0, m0, v0, wid, c)];
+  }
+
+  __device__ __forceinline__ void row(const H16Args &a, f32x4 (&acc)[S * TS][MC], const int pi,
+                                      int m0, int v0, int wid, int lane, float LDSP *colL) {
+    const int q = lane >> 4, c = lane & 15;
     const int mc = pi / S, s = pi % S;
     const int m = m0 + 16 * (MC * wid + mc) + c;
     const bool live = m < a.B;
@@ -260,125 +291,137 @@ __device__ __forceinline__ void hg16_epilogue(const H16Args &a,
     uint32_t mw[4] = {mwn[0], mwn[1], mwn[2], mwn[3]};
     const int act = actn;
     if (pi + 1 < NP) {
-      load_mask_raw<W32>(a, row_of(pi + 1), mwn);
-      actn = a.action[row_of(pi + 1)];
+      load_mask_raw<W32>(a, row_of(a, pi + 1, m0, v0, wid, c), mwn);
+      actn = a.action[row_of(a, pi + 1, m0, v0, wid, c)];
     }
     mask_fix<W32>(a, mw);
-    {
-      const int v = v0 + s;
-      if (v >= a.V) continue;  // workgroup-uniform: the last tile's missing segments
-      const int64_t row = (int64_t)mm * a.V + v;
-      const int tgt = (act >= 0 && act < a.A) ? act : -1;
-      // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
-      float xm[TS][4];
-      uint32_t nib[TS];
-      float mx = kPad;
+    const int v = v0 + s;
+    if (v >= a.V) return;  // workgroup-uniform: the last tile's missing segments
+    const int64_t row = (int64_t)mm * a.V + v;
+    const int tgt = (act >= 0 && act < a.A) ? act : -1;
+    // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
+    float xm[TS][4];
+    uint32_t nib[TS];
+    float mx = kPad;
 #pragma unroll
-      for (int u = 0; u < TS; u++) {
-        nib[u] = mw[u >> 1] >> (16 * (u & 1) + 4 * q);
+    for (int u = 0; u < TS; u++) {
+      nib[u] = mw[u >> 1] >> (16 * (u & 1) + 4 * q);
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int j = 16 * u + 4 * q + r;
-          const float x = ((nib[u] >> r) & 1u) ? kMasked : acc[s * TS + u][mc][r];
-          // TS = ceil(A / 16): only the segment's last tile reaches past A
-          xm[u][r] = (u < TS - 1 || j < a.A) ? x : kPad;
-          mx = fmaxf(mx, xm[u][r]);
-        }
+      for (int r = 0; r < 4; r++) {
+        const int j = 16 * u + 4 * q + r;
+        const float x = ((nib[u] >> r) & 1u) ? kMasked : acc[s * TS + u][mc][r];
+        // TS = ceil(A / 16): only the segment's last tile reaches past A
+        xm[u][r] = (u < TS - 1 || j < a.A) ? x : kPad;
+        mx = fmaxf(mx, xm[u][r]);
       }
-      mx = xmax(mx);
-      // pass 2: p = exp(x - m) (x - m first: exact at x = m, so an all-masked
-      // row gets p = 1 everywhere, as the unfused head), S, T = sum p x
-      float p[TS][4];
-      float Ss = 0.f, Ts = 0.f;
+    }
+    mx = xmax(mx);
+    // pass 2: p = exp(x - m) (x - m first: exact at x = m, so an all-masked
+    // row gets p = 1 everywhere, as the unfused head), S, T = sum p x
+    float p[TS][4];
+    float Ss = 0.f, Ts = 0.f;
+#pragma unroll
+    for (int u = 0; u < TS; u++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        p[u][r] = __builtin_amdgcn_exp2f((xm[u][r] - mx) * kLog2e);
+        Ss += p[u][r];
+        Ts = __builtin_fmaf(p[u][r], xm[u][r], Ts);
+      }
+    float xa = 0.f;
+    if (!BWD) {  // the given action's logit: tile u_t, register r_t of lane q_t
+      const int ut = tgt >> 4, rt = tgt & 3, qt = (tgt >> 2) & 3;
+      float sel[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int u = 0; u < TS; u++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          p[u][r] = __builtin_amdgcn_exp2f((xm[u][r] - mx) * kLog2e);
-          Ss += p[u][r];
-          Ts = __builtin_fmaf(p[u][r], xm[u][r], Ts);
-        }
-      float xa = 0.f;
-      if (!BWD) {  // the given action's logit: tile u_t, register r_t of lane q_t
-        const int ut = tgt >> 4, rt = tgt & 3, qt = (tgt >> 2) & 3;
-        float sel[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int u = 0; u < TS; u++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) sel[r] = u == ut ? xm[u][r] : sel[r];
-        xa = rt == 0 ? sel[0] : rt == 1 ? sel[1] : rt == 2 ? sel[2] : sel[3];
-        xa = (tgt >= 0 && q == qt) ? xa : 0.f;
+        for (int r = 0; r < 4; r++) sel[r] = u == ut ? xm[u][r] : sel[r];
+      xa = rt == 0 ? sel[0] : rt == 1 ? sel[1] : rt == 2 ? sel[2] : sel[3];
+      xa = (tgt >= 0 && q == qt) ? xa : 0.f;
+    }
+    Ss = xsum(Ss);
+    Ts = xsum(Ts);
+    const float lse = mx + logf(Ss);
+    const float inv = 1.0f / Ss;
+    const float H = lse - Ts * inv;  // Categorical.entropy, the tiled head's order
+    if (!BWD) {
+      xa = xsum(xa);  // one lane-element holds it, the others 0
+      if (live && q == 0) {
+        a.row_lp[row] = tgt >= 0 ? xa - lse : NAN;
+        a.row_ent[row] = H;
       }
-      Ss = xsum(Ss);
-      Ts = xsum(Ts);
-      const float lse = mx + logf(Ss);
-      const float inv = 1.0f / Ss;
-      const float H = lse - Ts * inv;  // Categorical.entropy, the tiled head's order
-      if (!BWD) {
-        xa = xsum(xa);  // one lane-element holds it, the others 0
-        if (live && q == 0) {
-          a.row_lp[row] = tgt >= 0 ? xa - lse : NAN;
-          a.row_ent[row] = H;
+    } else {
+      const float c1 = glp + gen * (H - lse);
+      // pass 1's per-element mask compares are recomputed from the nibbles
+      // here (kept live across pass 2 they are 64-bit SGPR pairs each, and
+      // spilled)
+#pragma unroll
+      for (int u = 0; u < TS; u++) asm volatile("" : "+v"(nib[u]));
+      int tq = tgt - 4 * q;
+      asm volatile("" : "+v"(tq));
+#pragma unroll
+      for (int u = 0; u < TS; u++) {
+        float d[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int j = 16 * u + 4 * q + r;
+          float dd = -(p[u][r] * inv) * __builtin_fmaf(gen, xm[u][r], c1);
+          dd += (16 * u + r == tq) ? glp : 0.f;
+          d[r] = ((u < TS - 1 || j < a.A) && !((nib[u] >> r) & 1u)) ? dd : 0.f;  // inner tiles: j < A
         }
-      } else {
-        const float c1 = glp + gen * (H - lse);
-        // pass 1's per-element mask compares are recomputed from the nibbles
-        // here (kept live across pass 2 they are 64-bit SGPR pairs each, and
-        // spilled)
+        if (colL) {
+          // the bias gradient db = 1^T dlogits (ppo.py:258-287 through the
+          // last Linear's bias): this row group's f32 column sums before the
+          // bf16 rounding, added to the wave's LDS sums by lane c = 15
+          float dl4[4];
 #pragma unroll
-        for (int u = 0; u < TS; u++) asm volatile("" : "+v"(nib[u]));
-        int tq = tgt - 4 * q;
-        asm volatile("" : "+v"(tq));
-#pragma unroll
-        for (int u = 0; u < TS; u++) {
-          float d[4];
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int j = 16 * u + 4 * q + r;
-            float dd = -(p[u][r] * inv) * __builtin_fmaf(gen, xm[u][r], c1);
-            dd += (16 * u + r == tq) ? glp : 0.f;
-            d[r] = ((u < TS - 1 || j < a.A) && !((nib[u] >> r) & 1u)) ? dd : 0.f;  // inner tiles: j < A
+          for (int r = 0; r < 4; r++) dl4[r] = live ? d[r] : 0.f;
+          const float cs = row16_colsum4(dl4, c);
+          if (c >= 12) colL[16 * (s * TS + u) + 4 * q + 2 * (c & 1) + ((c >> 1) & 1)] += cs;
+        }
+        // bf16 dlogits (round to nearest even), columns v A + j of row m
+        const int j0 = 16 * u + 4 * q;
+        const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
+        const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
+        const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
+        uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
+#ifdef VMP_HG16_NO_STORE  // timing-only build: no dlogits stores (outputs wrong)
+        asm volatile("" ::"v"(u0), "v"(u1), "v"(u2), "v"(u3));
+        continue;
+#endif
+        if (u < TS - 1 && ((a.A | a.ld) & 1) == 0) {
+          // the segment's inner tiles hold only real columns (TS = ceil(A / 16)):
+          // the lane's one condition is its sample
+          if (live) {
+            *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
+            *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
           }
-          if (colL) {
-            // the bias gradient db = 1^T dlogits (ppo.py:258-287 through the
-            // last Linear's bias): this row group's f32 column sums before the
-            // bf16 rounding, added to the wave's LDS sums by lane c = 15
-            float dl4[4];
-#pragma unroll
-            for (int r = 0; r < 4; r++) dl4[r] = live ? d[r] : 0.f;
-            const float cs = row16_colsum4(dl4, c);
-            if (c >= 12) colL[16 * (s * TS + u) + 4 * q + 2 * (c & 1) + ((c >> 1) & 1)] += cs;
-          }
-          // bf16 dlogits (round to nearest even), columns v A + j of row m
-          const int j0 = 16 * u + 4 * q;
-          const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
-          const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
-          const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
-          uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
-          if (u < TS - 1 && ((a.A | a.ld) & 1) == 0) {
-            // the segment's inner tiles hold only real columns (TS = ceil(A / 16)):
-            // the lane's one condition is its sample
-            if (live) {
-              *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
-              *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
-            }
-          } else if (((a.A | a.ld) & 1) == 0) {
-            // the last tile, even A / ld: j0 is a multiple of 4, so the lane's
-            // valid columns are 0, 2 or 4 and come in 4-B aligned pairs
-            if (live && j0 < a.A)
-              *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
-            if (live && j0 + 2 < a.A)
-              *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
-          } else if (live && j0 < a.A) {
-            dst[0] = u0;
-            if (j0 + 1 < a.A) dst[1] = u1;
-            if (j0 + 2 < a.A) dst[2] = u2;
-            if (j0 + 3 < a.A) dst[3] = u3;
-          }
+        } else if (((a.A | a.ld) & 1) == 0) {
+          // the last tile, even A / ld: j0 is a multiple of 4, so the lane's
+          // valid columns are 0, 2 or 4 and come in 4-B aligned pairs
+          if (live && j0 < a.A)
+            *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
+          if (live && j0 + 2 < a.A)
+            *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
+        } else if (live && j0 < a.A) {
+          dst[0] = u0;
+          if (j0 + 1 < a.A) dst[1] = u1;
+          if (j0 + 2 < a.A) dst[2] = u2;
+          if (j0 + 3 < a.A) dst[3] = u3;
         }
       }
     }
   }
+};
+
+template <int TS, bool BWD, int NW>
+__device__ __forceinline__ void hg16_epilogue(const H16Args &a,
+                                              f32x4 (&acc)[kMaxNT / TS * TS][16 / NW], int m0,
+                                              int v0, int wid, int lane, float LDSP *colL) {
+  Hg16Epi<TS, BWD, 16 / NW> ep;
+  ep.begin(a, m0, v0, wid, lane);
+#pragma unroll
+  for (int pi = 0; pi < Hg16Epi<TS, BWD, 16 / NW>::NP; pi++) ep.row(a, acc, pi, m0, v0, wid, lane, colL);
 }
 
 // The workgroup's bias-gradient partial: its waves' LDS column sums added in
@@ -506,6 +549,336 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   }
   if (dsum) hg16_dsum_flush<TS, NW>(a, biasL + BNp, v0, g);
 }
+
+// ---- the ping-pong kernel: two wave groups, one in the matrix loop while
+// the other runs its epilogue ----
+// The two-stage kernel's epilogue (a third of the forward, half of the
+// backward) runs on all 8 waves at once, so the matrix pipes idle through it.
+// Here the workgroup's M blocks are cut into halves of kHB = 128 samples;
+// group G (waves 4G..4G+3, one per SIMD) computes half blocks hb = G, G + 2,
+// ... and the groups are one half block apart in time: in the K steps of half
+// block hb (group hb & 1, the "main" group, MFMAs from LDS), the other group
+// runs the epilogue of half block hb - 1 out of its accumulators, its rows
+// spread over those K steps. Each SIMD then pairs one matrix wave with one
+// VALU wave (MI355X_MICROARCH.md "Two waves per SIMD": complementary segments
+// are what overlap). The main group stages the next K step (its own next, or
+// the other group's first) into the stage it does not read; it waits for its
+// own DMA before the step's barrier, the epilogue group waits for nothing
+// (its mask loads and dlogits stores stay in flight across barriers): raw
+// s_barrier, not __syncthreads, whose fence would drain them.
+constexpr int kHB = 128;  // samples per half block (4 waves x 2 columns of 16)
+#ifndef VMP_HG16P_ASM
+#define VMP_HG16P_ASM true  // the stage DMA through glds16_asm
+#endif
+
+//
+// NS LDS stages (2 or 3). At 3 the main group issues K step p + 2 in step p,
+// so a stage has two steps to land: in step p the main group waits for step
+// p + 1's pieces (its own from step p - 1; vmcnt(PW) leaves this step's PW
+// in flight) except in a half block's first step, where step p + 1 came from
+// the other group - which waits for it (vmcnt(0)) in its first epilogue step.
+template <int TS, bool BWD, int NS>
+__global__ __launch_bounds__(512, 2) void k_hg16p(H16Args a) {
+  constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
+  constexpr int MC = 2, kThreads = 512;
+  constexpr int kStageW = BNp * kRow, kStage = kStageW + kHB * kRow;
+  constexpr int PW = (BNp + kHB) / 8 / 4;  // pieces per main wave per stage
+  static_assert(((BNp + kHB) / 8) % 4 == 0, "stage pieces split evenly over 4 waves");
+  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
+  using Epi = Hg16Epi<TS, BWD, MC>;
+  constexpr int NP = Epi::NP;
+  extern __shared__ __align__(16) char lds_raw[];
+  char LDSP *lds = (char LDSP *)lds_raw;
+  float LDSP *biasL = reinterpret_cast<float LDSP *>(lds + NS * kStage);
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int grp = wid >> 2, wg = wid & 3;  // group, wave in group
+  const int q = lane >> 4, c = lane & 15;
+  int n_tile, g;
+  if (!hg16_tile(a, n_tile, g)) return;
+  const int v0 = n_tile * S;
+  const bool dsum = BWD && a.dpart;
+  float LDSP *colL = dsum ? biasL + BNp + wid * BNp : nullptr;
+  for (int n = t; n < BNp; n += kThreads) {
+    const int s = n / SA, j = n - s * SA, v = v0 + s;
+    biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
+  }
+  if (dsum)
+    for (int n = t; n < 8 * BNp; n += kThreads) biasL[BNp + n] = 0.f;
+  const int nk = a.K / kBK;
+  const int nblk = (a.m_blocks - g + a.m_groups - 1) / a.m_groups;
+  const int nhb = 2 * nblk, nst = nhb * nk;  // half blocks, K steps of all of them
+  auto half_m0 = [&](int hb) { return (g + (hb >> 1) * a.m_groups) * kBM + (hb & 1) * kHB; };
+  // global step st = K step st % nk of half block st / nk, in stage st % NS
+  auto issue4 = [&](int st) {
+    const int h = st / nk;
+    stage_issue<TS, NT, 4, kHB, VMP_HG16P_ASM>(a, lds + (st % NS) * kStage, v0, half_m0(h),
+                                               (st - h * nk) * kBK, wg, lane);
+  };
+  // the first NS - 1 steps, by all 8 waves
+#pragma unroll
+  for (int st = 0; st < NS - 1; st++) {
+    if (st < nst) {
+      const int h = st / nk;
+      stage_issue<TS, NT, 8, kHB, VMP_HG16P_ASM>(a, lds + st * kStage, v0, half_m0(h),
+                                                 (st - h * nk) * kBK, wid, lane);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x4 acc[NT][MC];
+  Epi ep;
+  int hb = 0, k = 0;  // phase p = hb nk + k: K step k of half block hb
+#pragma unroll 1
+  for (int p = 0; p < nst + nk; p++) {
+    if (hb < nhb && (hb & 1) == grp) {
+      // ---- main: K step k of half block hb ----
+      if (k == 0) {
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++) {
+          const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
+#pragma unroll
+          for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
+        }
+      }
+      const char LDSP *cur = lds + (p % NS) * kStage;
+      const bool issued = p + NS - 1 < nst;
+      if (issued) issue4(p + NS - 1);
+      const char LDSP *Hs = cur + kStageW;
+      constexpr int kPipe = VMP_HG16_PIPE, NF = 2 * NT;
+      bf16x8 hf[2][MC];
+#pragma unroll
+      for (int kk = 0; kk < 2; kk++)
+#pragma unroll
+        for (int mc = 0; mc < MC; mc++) hf[kk][mc] = frag(Hs, 16 * (MC * wg + mc) + c, 4 * kk + q);
+      bf16x8 wf[kPipe];
+#pragma unroll
+      for (int i = 0; i < kPipe; i++) wf[i] = frag(cur, 16 * (i % NT) + c, 4 * (i / NT) + q);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * MC + kPipe, 0);
+#pragma unroll
+      for (int i = 0; i < NF; i++) {
+        const int kk = i / NT, nt = i % NT;
+#pragma unroll
+        for (int mc = 0; mc < MC; mc++)
+          acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i % kPipe], hf[kk][mc], acc[nt][mc], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MC, 0);
+        if (i + kPipe < NF) {
+          const int j = i + kPipe;
+          wf[i % kPipe] = frag(cur, 16 * (j % NT) + c, 4 * (j / NT) + q);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+      if (NS == 2) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // The epilogue's cross-step loads (row prefetches, per-sample
+        // gradients) are dead here, but the compiler's wait analysis cannot
+        // see that this step never follows one of them with the load still in
+        // flight: had their registers been reused above, it would wait on
+        // vmcnt before that write - behind this step's stage DMA. Kept live
+        // (and read) only here, after the step's own wait, they are not reused.
+        ep.keep_live();
+      } else if (k > 0) {
+        if (issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else if (hb >= 1 && ((hb - 1) & 1) == grp) {
+      // NS = 3, the first epilogue step: the next step's stage is ours
+      if (NS == 3 && k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // ---- epilogue of half block hb - 1: rows [k NP / nk, (k + 1) NP / nk) ----
+      const int m0 = half_m0(hb - 1);
+#ifndef VMP_HG16_GEMM_ONLY
+      if (k == 0) ep.begin(a, m0, v0, wg, lane);
+      const int r0 = k * NP / nk, r1 = (k + 1) * NP / nk;
+#pragma unroll
+      for (int pi = 0; pi < NP; pi++)
+        if (pi >= r0 && pi < r1) ep.row(a, acc, pi, m0, v0, wg, lane, colL);
+#else
+      if (k == 0)
+#pragma unroll
+        for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+          for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
+#endif
+    }
+    // the stage read in this step may be overwritten from the next; the next
+    // step's stage has landed (the main group's vmcnt(0) above)
+    __builtin_amdgcn_s_barrier();
+    if (++k == nk) k = 0, hb++;
+  }
+  if (dsum) hg16_dsum_flush<TS, 8>(a, biasL + BNp, v0, g);
+}
+
+// ---- the resident-W kernel ----
+// The two-stage kernel stages W and h through LDS every K step: 60 LDS-DMA
+// pieces per step and workgroup, each holding its wave's issue for 100+
+// cycles (MI355X_MICROARCH.md, LDS-DMA piece issue cost), plus a barrier per
+// step - together they cap its matrix loop at ~45 % of the bf16 peak. Here a
+// workgroup's column tile is at most 128 columns (S = 8 / TS whole segments),
+// so its whole W slab (128 x K bf16, 128 KB at K = 512) is loaded into LDS
+// once and stays resident while the workgroup walks its M blocks; the h
+// operand, private to each wave (wave w owns samples 64 w .. 64 w + 63 of a
+// 512-sample block), is read from global memory straight into the MFMA
+// B-operand registers, RD K chunks of 32 ahead. The matrix loop has no
+// barrier and no DMA, so the 8 waves run free: one wave's epilogue (VALU,
+// dlogits stores) overlaps its SIMD partner's MFMAs.
+// W rows are 2K bytes; 16-B chunk c of row r sits at chunk c ^ (r & SW) (SW
+// 15, or 7 at K = 64): the ds_read_b128 fragment groups hit 16 distinct bank
+// quads. XCD-aware walk (hg16r_tile): the workgroups resident on one XCD take
+// different column tiles and the same M group, so each h block is read from
+// HBM about once per XCD and from L2 by the others.
+constexpr int kRBM = 512;  // samples per M block (8 waves x 4 columns of 16)
+constexpr int kRMC = 4;    // 16-sample columns per wave
+
+template <int TS>
+constexpr int res_seg() { return 8 / TS; }  // segments per column tile
+
+// the workgroup's column tile and M group (false: a padding workgroup)
+__device__ __forceinline__ bool hg16r_tile(const H16Args &a, int &n_tile, int &g) {
+  const int b = blockIdx.x, xcd = b & 7, i = b >> 3;
+  n_tile = i % a.n_tiles;
+  g = (i / a.n_tiles) * 8 + xcd;
+  return g < a.m_groups && g < a.m_blocks;
+}
+
+template <int TS, bool BWD, int RD>
+__global__ __launch_bounds__(512, 2) void k_hg16r(H16Args a) {
+  constexpr int S = res_seg<TS>(), NT = S * TS, SA = 16 * TS, BN = 16 * NT, MC = kRMC;
+  using Epi = Hg16Epi<TS, BWD, MC, S>;
+  extern __shared__ __align__(16) char lds_raw[];
+  char LDSP *Wl = (char LDSP *)lds_raw;
+  const int K = a.K, rowb = 2 * K;
+  float LDSP *biasL = reinterpret_cast<float LDSP *>(Wl + (size_t)BN * rowb);
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int q = lane >> 4, c = lane & 15;
+  int n_tile, g;
+  if (!hg16r_tile(a, n_tile, g)) return;
+  const int v0 = n_tile * S;
+  const bool dsum = BWD && a.dpart;
+  float LDSP *colL = dsum ? biasL + BN + wid * BN : nullptr;
+  const int sw = K >= 128 ? 15 : 7;
+  // ---- W slab -> LDS, once: piece p = LDS bytes [1 KB p, 1 KB (p + 1)) ----
+  {
+    const int pieces = BN * rowb / 1024;
+    for (int p = wid; p < pieces; p += 8) {
+      const int pos = p * 1024 + 16 * lane;
+      const int r = pos / rowb, pc = (pos - r * rowb) >> 4;
+      const int sg = r / SA, j = r - sg * SA, v = v0 + sg;
+      const int wr = (v < a.V && j < a.A) ? v * a.A + j : v0 * a.A;  // pad rows: any row
+      const uint16_t *src = a.w + (int64_t)wr * K + 8 * (pc ^ (r & sw));
+      __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)(Wl + p * 1024), 16, 0, 0);
+    }
+  }
+  for (int n = t; n < BN; n += 512) {
+    const int sg = n / SA, j = n - sg * SA, v = v0 + sg;
+    biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
+  }
+  if (dsum)
+    for (int n = t; n < 8 * BN; n += 512) biasL[BN + n] = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int nkc = K / 32;  // K chunks of one MFMA each
+  // this lane's W fragment offsets (row 16 nt + c, logical chunk 4 kc + q)
+  const int wrow = c * rowb;
+  // the walk: blocks g + G t, t = 0 .. nblk - 1, started at t0 = (n_tile %
+  // stag) nblk / stag and wrapped, so the XCD's workgroups (consecutive
+  // column tiles, one M group) are spread over stag blocks: a block's h
+  // chunks miss in L2 for the first group to reach it only, instead of for
+  // all 32 workgroups at once (lockstep walks wait on the same misses)
+  const int nblk = (a.m_blocks - g + a.m_groups - 1) / a.m_groups;
+  const int t0 = a.stag > 1 ? (n_tile % a.stag) * nblk / a.stag : 0;
+#pragma unroll 1
+  for (int tt = 0; tt < nblk; tt++) {
+    const int t = tt + t0 < nblk ? tt + t0 : tt + t0 - nblk;
+    const int mb = g + t * a.m_groups;
+    const int m0 = mb * kRBM;
+    const uint16_t *hp[MC];
+#pragma unroll
+    for (int mc = 0; mc < MC; mc++) {
+      const int m = m0 + 16 * (MC * wid + mc) + c;
+      hp[mc] = a.h + (int64_t)(m < a.B ? m : a.B - 1) * K + 8 * q;
+    }
+    f32x4 acc[NT][MC];
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
+#pragma unroll
+      for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
+    }
+    bf16x8 hr[RD][MC];  // h fragments of K chunks kc .. kc + RD - 1
+#pragma unroll
+    for (int d = 0; d < RD - 1; d++)
+#pragma unroll
+      for (int mc = 0; mc < MC; mc++) hr[d][mc] = *reinterpret_cast<const bf16x8 *>(hp[mc] + 32 * d);
+    // W fragments run kPipe ahead of their MFMAs in the flattened (chunk,
+    // tile) order, across the RD-chunk loop's back edge too; the
+    // sched_group_barriers pin {MC MFMAs, one ds_read} so the reads are not
+    // sunk to their use (one read ahead, each read's latency was exposed)
+    constexpr int NF = RD * NT, kPipe = NF % 4 == 0 ? 4 : 2;
+    static_assert(NF % kPipe == 0, "the W pipeline rotates with the loop");
+    auto wfrag = [&](int kc, int nt) {
+      return *reinterpret_cast<const bf16x8 LDSP *>(Wl + wrow + 16 * nt * rowb +
+                                                    (((4 * kc + q) ^ (c & sw)) << 4));
+    };
+    bf16x8 wf[kPipe];
+#pragma unroll
+    for (int i = 0; i < kPipe; i++) wf[i] = wfrag(i / NT, i % NT);
+#pragma unroll 1
+    for (int kc0 = 0; kc0 < nkc; kc0 += RD) {
+      const bool more = kc0 + RD < nkc;
+#pragma unroll
+      for (int i = 0; i < NF; i++) {
+        const int d = i / NT, nt = i % NT;
+        if (nt == 0 && kc0 + d + RD - 1 < nkc) {
+          // chunk kc + RD - 1 into the slot chunk kc - 1 used
+#pragma unroll
+          for (int mc = 0; mc < MC; mc++)
+            hr[(d + RD - 1) % RD][mc] =
+                *reinterpret_cast<const bf16x8 *>(hp[mc] + 32 * (kc0 + d + RD - 1));
+        }
+#pragma unroll
+        for (int mc = 0; mc < MC; mc++)
+          acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i % kPipe], hr[d][mc], acc[nt][mc], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, MC, 0);
+        const int j = i + kPipe;
+        if (j < NF) {
+          wf[i % kPipe] = wfrag(kc0 + j / NT, j % NT);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        } else if (more) {
+          wf[i % kPipe] = wfrag(kc0 + RD + (j - NF) / NT, (j - NF) % NT);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      }
+    }
+#ifdef VMP_HG16_GEMM_ONLY
+#pragma unroll
+    for (int nt = 0; nt < NT; nt++)
+#pragma unroll
+      for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
+#else
+    Epi ep;
+    ep.begin(a, m0, v0, wid, lane);
+#pragma unroll
+    for (int pi = 0; pi < Epi::NP; pi++) ep.row(a, acc, pi, m0, v0, wid, lane, colL);
+#endif
+  }
+  if (dsum) {  // the workgroup's bias-gradient partial, waves in order
+    __syncthreads();
+    for (int n = t; n < BN; n += 512) {
+      const int sg = n / SA, j = n - sg * SA, v = v0 + sg;
+      float x = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; w++) x += biasL[BN + w * BN + n];
+      if (v < a.V && j < a.A) a.dpart[(int64_t)g * a.V * a.A + v * a.A + j] = x;
+    }
+  }
+}
+
+template <int TS>
+constexpr size_t res_lds_fixed() {  // bytes besides the W slab: bias + 8 waves' column sums
+  return 9 * 16 * (res_seg<TS>() * TS) * sizeof(float);
+}
+template <int TS>
+size_t res_lds_bytes(int K) { return (size_t)16 * res_seg<TS>() * TS * 2 * K + res_lds_fixed<TS>(); }
 
 // ---- the deep-pipeline kernel: BK = 32 (64-B rows), NS LDS stages ----
 // One stage is (BNp + BM) rows x 64 B (30 KB at NT = 14), so NS - 1 stages are
@@ -656,10 +1029,15 @@ constexpr size_t lds_bytes() {
   return 2 * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
 }
 template <int TS, int NS>
+constexpr size_t lds_bytes_pp() {
+  return NS * (size_t)(16 * (kMaxNT / TS * TS) + kHB) * kRow + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
+}
+template <int TS, int NS>
 constexpr size_t lds_bytes_deep() {
   return NS * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow2 + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
 }
 static_assert(lds_bytes<1>() <= 160 * 1024, "stages exceed LDS");
+static_assert(lds_bytes_pp<1, 3>() <= 160 * 1024, "ping-pong stages exceed LDS");
 #ifndef VMP_HG16_NS
 #define VMP_HG16_NS 4  // deep kernel's LDS stages
 #endif
@@ -705,6 +1083,23 @@ hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
     }
     return hipGetLastError();
   }
+  // VMP_HG16_PP=2 / 3: the ping-pong kernel with 2 / 3 LDS stages
+  const char *pp = getenv("VMP_HG16_PP");
+  if (pp && (pp[0] == '2' || pp[0] == '3')) {  // its LDS stages
+    const bool s3 = pp[0] == '3';
+    switch (TS) {
+#define VMP_HG16P_CASE(T)                                                                        \
+  case T:                                                                                        \
+    if (s3) hipLaunchKernelGGL((k_hg16p<T, BWD, 3>), grid, dim3(512), (lds_bytes_pp<T, 3>()), st, a); \
+    else hipLaunchKernelGGL((k_hg16p<T, BWD, 2>), grid, dim3(512), (lds_bytes_pp<T, 2>()), st, a);    \
+    break;
+      VMP_HG16P_CASE(1) VMP_HG16P_CASE(2) VMP_HG16P_CASE(3) VMP_HG16P_CASE(4)
+      VMP_HG16P_CASE(5) VMP_HG16P_CASE(6) VMP_HG16P_CASE(7)
+      default: VMP_HG16P_CASE(8)
+#undef VMP_HG16P_CASE
+    }
+    return hipGetLastError();
+  }
   switch (TS) {
 #define VMP_HG16_CASE(T) \
   case T: hipLaunchKernelGGL((k_hg16<T, BWD, NW>), grid, block, lds_bytes<T>(), st, a); break;
@@ -716,9 +1111,59 @@ hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
   return hipGetLastError();
 }
 
+// The resident-W kernel when its slab fits LDS: S = 8 / TS segments per
+// column tile, 512-sample M blocks, G M groups (a multiple of 8, one XCD's
+// workgroups per group at a time) whose n_tiles x G workgroups fill the last
+// one-per-CU dispatch round best.
+template <bool BWD>
+bool launch_res(H16Args &a, int TS, hipStream_t st, hipError_t &err) {
+  const char *rs = getenv("VMP_HG16_RES");
+  if (!(rs && rs[0] == '1')) return false;
+  const int S = 8 / TS;
+  const size_t lds = (size_t)16 * S * TS * 2 * a.K + 9 * 16 * S * TS * sizeof(float);
+  if (lds > 160 * 1024) return false;
+  a.n_tiles = (a.V + S - 1) / S;
+  a.m_blocks = (a.B + kRBM - 1) / kRBM;
+  int best = 8;
+  double best_eff = -1.0;
+  for (int G = 8; G <= 512 && (G <= a.m_blocks || G == 8); G += 8) {
+    const int64_t wg = (int64_t)a.n_tiles * G;
+    const double eff = (double)wg / ((double)((wg + 255) / 256) * 256.0);
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = G;
+    }
+    if (eff > 0.97) break;
+  }
+  a.m_groups = best;
+  a.team = 0;
+  const char *sg = getenv("VMP_HG16_STAG");
+  a.stag = sg ? atoi(sg) : 4;
+  const dim3 grid((unsigned)((int64_t)a.n_tiles * best)), block(512);
+  const char *rde = getenv("VMP_HG16_RD");  // h chunks in flight: 2 (default) or 4 (spills)
+  const bool rd4 = (a.K / 32) % 4 == 0 && rde && rde[0] == '4';
+  switch (TS) {
+#define VMP_HG16R_CASE(T)                                                              \
+  case T:                                                                              \
+    if (rd4) hipLaunchKernelGGL((k_hg16r<T, BWD, 4>), grid, block, lds, st, a);        \
+    else hipLaunchKernelGGL((k_hg16r<T, BWD, 2>), grid, block, lds, st, a);            \
+    break;
+    VMP_HG16R_CASE(1) VMP_HG16R_CASE(2) VMP_HG16R_CASE(3) VMP_HG16R_CASE(4)
+    VMP_HG16R_CASE(5) VMP_HG16R_CASE(6) VMP_HG16R_CASE(7)
+    default: VMP_HG16R_CASE(8)
+#undef VMP_HG16R_CASE
+  }
+  err = hipGetLastError();
+  return true;
+}
+
 template <bool BWD>
 hipError_t launch_hg16(H16Args &a, hipStream_t st) {
   const int TS = pick_ts(a.A);
+  {
+    hipError_t e;
+    if (launch_res<BWD>(a, TS, st, e)) return e;
+  }
   const int S = kMaxNT / TS;
   a.n_tiles = (a.V + S - 1) / S;
   a.m_blocks = (a.B + kBM - 1) / kBM;
