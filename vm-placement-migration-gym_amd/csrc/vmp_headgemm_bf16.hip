@@ -69,6 +69,7 @@ struct H16Args {
   int B, K, V, A, W32, n_tiles, m_blocks, m_groups, ld;
   int team, teams;  // XCD teams (launch_hg16); team 0: one column tile per block index
   int stag;         // resident-W kernel: block-walk stagger (hg16r walk)
+  int skew;         // two-stage kernel: start delay of every other workgroup, in s_sleep 127 units
   const uint16_t *h, *w;
   const float *bias;
   const uint32_t *bits;
@@ -239,6 +240,42 @@ __device__ __forceinline__ float row16_colsum4(const float (&d)[4], int c) {
 // K steps, so the state between rows is these few registers and acc).
 // colL (backward with a.dpart, else null): the wave's f32 column sums of
 // dlogits over every sample it has processed, one float per tile column.
+typedef uint32_t u32x2u __attribute__((ext_vector_type(2), aligned(4)));
+
+// One tile's bf16 dlogits of one lane, pk0 = columns j0, j0 + 1 and pk1 =
+// j0 + 2, j0 + 3 (j0 = 16 u + 4 q) of sample m, VM row v. Even A and ld:
+// the lane's 8 bytes go out as one dwordx2 (4-byte aligned: the unaligned
+// access mode of the HSA targets; two dword stores per tile were a third of
+// the backward's store instructions' issue time).
+template <int TS>
+__device__ __forceinline__ void store_dl_tile(const H16Args &a, int m, int v, int u, int q,
+                                              uint32_t pk0, uint32_t pk1) {
+  const bool live = m < a.B;
+  const int j0 = 16 * u + 4 * q;
+  uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
+  if (((a.A | a.ld) & 1) == 0) {
+    // inner tiles hold only real columns (TS = ceil(A / 16)); in the last
+    // one j0 is a multiple of 4, so a lane's valid columns are 0, 2 or 4
+#ifdef VMP_HG16_OLDST  // A/B: two dword stores per tile
+    if (live && (u < TS - 1 || j0 + 2 < a.A)) {
+      *reinterpret_cast<uint32_t *>(dst) = pk0;
+      *reinterpret_cast<uint32_t *>(dst + 2) = pk1;
+    } else if (live && j0 < a.A) {
+#else
+    if (live && (u < TS - 1 || j0 + 2 < a.A)) {
+      *reinterpret_cast<u32x2u *>(dst) = u32x2u{pk0, pk1};
+    } else if (live && j0 < a.A) {
+#endif
+      *reinterpret_cast<uint32_t *>(dst) = pk0;
+    }
+  } else if (live && j0 < a.A) {
+    dst[0] = (uint16_t)pk0;
+    if (j0 + 1 < a.A) dst[1] = (uint16_t)(pk0 >> 16);
+    if (j0 + 2 < a.A) dst[2] = (uint16_t)pk1;
+    if (j0 + 3 < a.A) dst[3] = (uint16_t)(pk1 >> 16);
+  }
+}
+
 template <int TS, bool BWD, int MC, int SEG = kMaxNT / TS>
 struct Hg16Epi {
   static constexpr int S = SEG, NP = MC * S;  // S segments of TS tiles per column tile
@@ -380,35 +417,16 @@ struct Hg16Epi {
           if (c >= 12) colL[16 * (s * TS + u) + 4 * q + 2 * (c & 1) + ((c >> 1) & 1)] += cs;
         }
         // bf16 dlogits (round to nearest even), columns v A + j of row m
-        const int j0 = 16 * u + 4 * q;
         const __bf16 b0 = (__bf16)d[0], b1 = (__bf16)d[1], b2 = (__bf16)d[2], b3 = (__bf16)d[3];
-        const uint16_t u0 = __builtin_bit_cast(uint16_t, b0), u1 = __builtin_bit_cast(uint16_t, b1);
-        const uint16_t u2 = __builtin_bit_cast(uint16_t, b2), u3 = __builtin_bit_cast(uint16_t, b3);
-        uint16_t *dst = a.dl + (int64_t)m * a.ld + (int64_t)v * a.A + j0;
+        const uint32_t pk0 = (uint32_t)__builtin_bit_cast(uint16_t, b0) |
+                             ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
+        const uint32_t pk1 = (uint32_t)__builtin_bit_cast(uint16_t, b2) |
+                             ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16);
 #ifdef VMP_HG16_NO_STORE  // timing-only build: no dlogits stores (outputs wrong)
-        asm volatile("" ::"v"(u0), "v"(u1), "v"(u2), "v"(u3));
+        asm volatile("" ::"v"(pk0), "v"(pk1));
         continue;
 #endif
-        if (u < TS - 1 && ((a.A | a.ld) & 1) == 0) {
-          // the segment's inner tiles hold only real columns (TS = ceil(A / 16)):
-          // the lane's one condition is its sample
-          if (live) {
-            *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
-            *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
-          }
-        } else if (((a.A | a.ld) & 1) == 0) {
-          // the last tile, even A / ld: j0 is a multiple of 4, so the lane's
-          // valid columns are 0, 2 or 4 and come in 4-B aligned pairs
-          if (live && j0 < a.A)
-            *reinterpret_cast<uint32_t *>(dst) = (uint32_t)u0 | ((uint32_t)u1 << 16);
-          if (live && j0 + 2 < a.A)
-            *reinterpret_cast<uint32_t *>(dst + 2) = (uint32_t)u2 | ((uint32_t)u3 << 16);
-        } else if (live && j0 < a.A) {
-          dst[0] = u0;
-          if (j0 + 1 < a.A) dst[1] = u1;
-          if (j0 + 2 < a.A) dst[2] = u2;
-          if (j0 + 3 < a.A) dst[3] = u3;
-        }
+        store_dl_tile<TS>(a, m, v, u, q, pk0, pk1);
       }
     }
   }
@@ -465,6 +483,12 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   const int q = lane >> 4, c = lane & 15;
   int n_tile, g;
   if (!hg16_tile(a, n_tile, g)) return;
+  // workgroups of equal work start together and stay in step, so every CU's
+  // epilogue (VALU, and the backward's dlogits stores at the HBM write rate)
+  // fell in the same window; every other workgroup of an XCD starts a
+  // fraction of a block later
+  if (a.skew > 0 && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < a.skew; i++) __builtin_amdgcn_s_sleep(127);
   const int v0 = n_tile * S;
   const bool dsum = BWD && a.dpart;  // backward: the bias gradient's column sums too
   float LDSP *colL = dsum ? biasL + BNp + wid * BNp : nullptr;
@@ -1191,6 +1215,8 @@ hipError_t launch_hg16(H16Args &a, hipStream_t st) {
   } else {
     a.m_groups = pick_groups(a.n_tiles, a.m_blocks);
   }
+  const char *sk = getenv("VMP_HG16_SKEW");
+  a.skew = sk ? atoi(sk) : 0;
   return launch_ts<BWD, 8>(a, TS, st);
 }
 
