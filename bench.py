@@ -550,24 +550,30 @@ def cpu_baseline(cfg, threads=0, what="", envs_per_thread=16):
     process may run on (the affinity set, capped by the cgroup's CPU quota when
     one is set: threads beyond the quota only time-slice), 16 envs per thread
     (envs_per_thread),
-    warmed up 2 500 steps (the GPU window's env ages), then 3 timed passes of
-    1 000 steps (one service period each); value = the median pass, spread =
-    (max - min) / median."""
+    warmed up 2 500 steps (the GPU window's env ages), then 7 timed passes of
+    1 000 steps (one service period each) after an untimed one; value = the
+    median pass, spread = (max - min) / median, spread_trimmed the same
+    without the extreme passes."""
     from oracle import oracle as O
     host = host_cpus()
     if not threads:
         threads = host["affinity"]
         if host["cgroup_quota_cores"]:
             threads = max(1, min(threads, int(host["cgroup_quota_cores"])))
-    n_env, warm, steps, reps = envs_per_thread * threads, 2500, 1000, 5
+    n_env, warm, steps, reps = envs_per_thread * threads, 2500, 1000, 7
     # one more pass than reported: the first pass after the warm-up steps is
     # untimed warm-up of its own (it ran up to 7 % slow on a shared host)
     secs, _ = O.rollout_timed(cfg, n_env, 0, 4, warm, steps, 0, threads, eval_mode=False,
                               reps=reps + 1)
     rates = n_env * steps / secs[1:]
     med = float(np.median(rates))
+    srt = np.sort(rates)
     return {"value": med, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "repeats": [float(x) for x in rates], "spread": float((rates.max() - rates.min()) / med),
+            # the same without the slowest and the fastest pass: one pass
+            # caught by a neighbour's load on the shared host moves `spread`
+            # alone (tools/cpu_spread.py on the GPU box: 1-2 % at 16 threads)
+            "spread_trimmed": float((srt[-2] - srt[1]) / med),
             "warmup_pass": float(n_env * steps / secs[0]),
             **host,
             "sample": f"{n_env} envs x {steps} FirstFit act+step per pass, {reps} passes (median) "

@@ -69,7 +69,6 @@ struct H16Args {
   int B, K, V, A, W32, n_tiles, m_blocks, m_groups, ld;
   int team, teams;  // XCD teams (launch_hg16); team 0: one column tile per block index
   int stag;         // resident-W kernel: block-walk stagger (hg16r walk)
-  int skew;         // two-stage kernel: start delay of every other workgroup, in s_sleep 127 units
   const uint16_t *h, *w;
   const float *bias;
   const uint32_t *bits;
@@ -483,12 +482,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   const int q = lane >> 4, c = lane & 15;
   int n_tile, g;
   if (!hg16_tile(a, n_tile, g)) return;
-  // workgroups of equal work start together and stay in step, so every CU's
-  // epilogue (VALU, and the backward's dlogits stores at the HBM write rate)
-  // fell in the same window; every other workgroup of an XCD starts a
-  // fraction of a block later
-  if (a.skew > 0 && ((blockIdx.x >> 3) & 1))
-    for (int i = 0; i < a.skew; i++) __builtin_amdgcn_s_sleep(127);
   const int v0 = n_tile * S;
   const bool dsum = BWD && a.dpart;  // backward: the bias gradient's column sums too
   float LDSP *colL = dsum ? biasL + BNp + wid * BNp : nullptr;
@@ -1215,8 +1208,6 @@ hipError_t launch_hg16(H16Args &a, hipStream_t st) {
   } else {
     a.m_groups = pick_groups(a.n_tiles, a.m_blocks);
   }
-  const char *sk = getenv("VMP_HG16_SKEW");
-  a.skew = sk ? atoi(sk) : 0;
   return launch_ts<BWD, 8>(a, TS, st);
 }
 
