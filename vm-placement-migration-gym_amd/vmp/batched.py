@@ -100,9 +100,12 @@ class BatchedVmEnv:
         check(lib().vmp_reset(h, ptr(s), ptr(m), ptr(o)))
         return o
 
-    def step(self, actions, obs=None, reward=None, done=None, valid=None, want_valid=True):
+    def step(self, actions, obs=None, reward=None, done=None, valid=None, want_valid=True,
+             bool_done=True):
         """One VmEnv.step per env. actions: int tensor [N, V] on the device.
-        Returns (obs f32[N,D], reward f64[N], done bool[N], valid u8[N,V])."""
+        Returns (obs f32[N,D], reward f64[N], done bool[N], valid u8[N,V]);
+        bool_done=False returns the u8 done buffer itself (no conversion
+        kernel: a captured step graph reads `done` in place)."""
         h = self._bind()
         a = actions
         if a.dtype != torch.int32 or not a.is_contiguous() or a.device != self.device:
@@ -115,7 +118,7 @@ class BatchedVmEnv:
         if want_valid and valid is None:
             valid = self._empty((self.n_envs, self.V), torch.uint8)
         check(lib().vmp_step(h, ptr(a), ptr(obs), ptr(reward), ptr(done), ptr(valid)))
-        return obs, reward, done.bool(), valid
+        return obs, reward, done.bool() if bool_done else done, valid
 
     def heuristic_act(self, policy="firstfit"):
         """FirstFitAgent.act / BestFitAgent.act for every env -> int32 [N, V]."""

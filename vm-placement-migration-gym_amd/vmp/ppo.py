@@ -432,7 +432,8 @@ class ActStepGraph:
     def _step(self):
         self.env.mask_bits(out=self.bits)
         a = self.agent.act_batch(self.obs, self.bits)
-        self.env.step(a, obs=self.obs, reward=self.reward, done=self.done, want_valid=False)
+        self.env.step(a, obs=self.obs, reward=self.reward, done=self.done, want_valid=False,
+                      bool_done=False)
         self.actions = a  # the captured step's action buffer: the last replay's actions
 
     def replay(self):
@@ -667,7 +668,8 @@ class PPOTrainer:
             self.act[t].copy_(act)
             self.logp[t].copy_(lp)
             nxt = self.obs[t + 1] if t + 1 < T else self.last_obs
-            env.step(act, obs=nxt, reward=self.r64, done=self.d8, want_valid=False)
+            env.step(act, obs=nxt, reward=self.r64, done=self.d8, want_valid=False,
+                     bool_done=False)
             self.ep_ret.add_(self.r64)
             r = self._scale_reward(self.r64) if cfg.reward_scaling else self.r64
             self.rew[t].copy_(r)
