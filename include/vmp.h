@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 9
+#define VMP_ABI_VERSION 10
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -289,6 +289,21 @@ int vmp_actor_head_bf16_fwd(int32_t B, int32_t K, int32_t V, int32_t A, const ui
                             const uint16_t *weight, const float *bias, const uint32_t *mask_bits,
                             const int32_t *action, float *logprob, float *entropy,
                             float *workspace, void *hip_stream);
+/* Rollout sampling on the same kernel (the bf16 leg's collect: get_action(obs,
+ * mask) ppo.py:115-126 and PPOAgent.act's WAIT coin ppo.py:151-156, as
+ * vmp_policy_head / vmp_actor_head in VMP_HEAD_SAMPLE mode): action
+ * i32[B][V] is the OUTPUT, drawn per (sample, VM row) by inverse CDF over
+ * the masked softmax in action order with the counter-based uniform of
+ * vmp_policy_head's stream (seed, offset + b*V + v; rng_counter nullable,
+ * mixed into the seed as there); wait_ratio >= 0 applies the WAIT coin at
+ * column wait_index (needs mask_bits). logprob / entropy f32[B] of the drawn
+ * actions. The logits never reach memory. (ABI 10) */
+int vmp_actor_head_bf16_sample(int32_t B, int32_t K, int32_t V, int32_t A, const uint16_t *h,
+                               const uint16_t *weight, const float *bias,
+                               const uint32_t *mask_bits, float wait_ratio, int32_t wait_index,
+                               uint64_t seed, uint64_t offset, const uint64_t *rng_counter,
+                               int32_t *action, float *logprob, float *entropy, float *workspace,
+                               void *hip_stream);
 /* Backward: recomputes the logits tiles and writes
  *   dlogits[b][ld] = bf16(d logprob/entropy loss / d logits)  (ld >= V*A)
  * with g_logprob / g_entropy f32[B] (nullable: 0), masked entries 0, as

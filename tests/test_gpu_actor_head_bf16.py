@@ -188,6 +188,78 @@ def test_resident_w_kernel_matches_two_stage(monkeypatch, B, K, V, A, rd):
     torch.testing.assert_close(outs[1][3], outs[0][3], rtol=1e-5, atol=1e-6 * B)
 
 
+@pytest.mark.parametrize("B,K,V,A", [(1500, 512, 300, 102), (700, 256, 13, 39),
+                                     (333, 64, 7, 22), (300, 128, 5, 128)])
+def test_bf16_sample_matches_given_mode(B, K, V, A):
+    """SAMPLE mode (vmp_actor_head_bf16_sample): every drawn action is a valid
+    one (an all-masked row draws from all A), and the returned logprob /
+    entropy are bit-identical to the GIVEN-mode forward of those actions (the
+    same logits tiles, the same lse / entropy arithmetic)."""
+    from vmp import head as H
+    h, w, b, mask, _ = _case(B, K, V, A, seed=7 * B + A)
+    bits = H.pack_mask(mask, V, A)
+    hb, wb = h.bfloat16(), w.bfloat16()
+    act, lp, ent = H.actor_head_bf16_sample(hb, wb, b, V, A, bits, H.HeadRng(5))
+    torch.cuda.synchronize()
+    assert act.dtype == torch.int32 and tuple(act.shape) == (B, V)
+    a64 = act.long()
+    assert bool(((a64 >= 0) & (a64 < A)).all())
+    picked_masked = mask.gather(2, a64[..., None])[..., 0]
+    all_masked = mask.all(-1)
+    assert not bool((picked_masked & ~all_masked).any())
+    _, lp_g, ent_g = H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act)
+    assert torch.equal(lp, lp_g) and torch.equal(ent, ent_g)
+
+
+def test_bf16_sample_law_and_wait_coin():
+    """The draw's law: 8 192 samples with the same hidden state give each VM
+    row 8 192 draws; their frequencies match the masked softmax of the
+    fp32 logits on the bf16-rounded operands (plain PyTorch) within 5 sigma.
+    WAIT coin (PPOAgent.act, ppo.py:151-156): wait_ratio 1 never forbids WAIT
+    (the draws equal the coin-less ones), wait_ratio 0 always does where more
+    than one action is invalid."""
+    from vmp import head as H
+    B, K, V, A = 8192, 128, 6, 20
+    g = torch.Generator().manual_seed(3)
+    h1 = torch.tanh(torch.randn((1, K), generator=g))
+    w = torch.randn((V * A, K), generator=g) * (1.0 / K ** 0.5)
+    b = torch.randn((V * A,), generator=g) * 0.3
+    m1 = torch.rand((1, V, A), generator=g) < 0.3
+    m1[0, 0] = True          # all masked: uniform over A
+    m1[0, 1, :] = False      # nothing masked
+    m1[0, 2, :] = True
+    m1[0, 2, A - 2] = False  # one valid action
+    h = h1.expand(B, K).contiguous().to(DEV)
+    mask = m1.expand(B, V, A).contiguous().to(DEV)
+    bits = H.pack_mask(mask, V, A)
+    hb, wb, bd = h.bfloat16(), w.to(DEV).bfloat16(), b.to(DEV)
+    act, _, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, H.HeadRng(11))
+    logits = torch.addmm(bd, hb[:1].float(), wb.float().t()).reshape(V, A)
+    logits = logits.masked_fill(mask[0], -1e7)
+    prob = torch.softmax(logits.double(), -1)
+    freq = torch.stack([torch.bincount(act[:, v].long(), minlength=A) for v in range(V)]).double() / B
+    sigma = (prob * (1 - prob) / B).sqrt()
+    assert bool(((freq - prob).abs() <= 5 * sigma + 1e-12).all()), (freq - prob).abs().max()
+    P = A - 2  # the WAIT column of this case
+    a_none, lp_none, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, H.HeadRng(12))
+    a_one, lp_one, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, H.HeadRng(12),
+                                                wait_ratio=1.0, wait_index=P)
+    assert torch.equal(a_none, a_one) and torch.equal(lp_none, lp_one)
+    a_zero, _, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, H.HeadRng(12),
+                                            wait_ratio=0.0, wait_index=P)
+    inval = mask[0].sum(-1)  # per VM row: invalid actions
+    for v in range(V):
+        # (WAIT the only valid action: forbidding it masks the whole row,
+        # which then draws uniformly over A, as the reference's Categorical)
+        if int(inval[v]) > 1 and not bool(mask[0, v, P]) and A - int(inval[v]) > 1:
+            assert not bool((a_zero[:, v] == P).any()), v
+    # a device counter (captured graphs) moves the stream on every call
+    rng = H.HeadRng(13).graph_counter(DEV)
+    a1, _, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, rng)
+    a2, _, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, rng)
+    assert int(rng.counter.item()) == 2 and not torch.equal(a1, a2)
+
+
 def test_no_mask_and_deterministic():
     """bits = None (masked=False in PPOConfig) and run-to-run identical outputs."""
     B, K, V, A = 777, 512, 300, 102

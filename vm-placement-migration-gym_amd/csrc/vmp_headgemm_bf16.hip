@@ -77,7 +77,31 @@ struct H16Args {
   float *row_lp, *row_ent;  // forward: per (sample, VM row)
   uint16_t *dl;             // backward: bf16 dlogits [B][ld]
   float *dpart;             // backward, nullable: bias-gradient partials [M group][V*A]
+  // sampling (vmp_actor_head_bf16_sample): action is the output [B][V]; the
+  // launch seed is seed, mixed with *ctr when ctr is set (vmp_policy.hip's
+  // stream); wait_ratio >= 0: PPOAgent.act's WAIT coin per row
+  uint64_t seed, offset;
+  const uint64_t *ctr;
+  float wait_ratio;
+  int wait_index;
+  int32_t *act_out;  // sampling: the drawn actions [B][V]
 };
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+// the counter-based uniforms of vmp_policy.hip / vmp_headgemm.hip (stream
+// (seed, ctr), 24 random bits)
+__device__ __forceinline__ float uniform_at(uint64_t seed, uint64_t ctr) {
+  const uint64_t h = mix64(seed ^ mix64(ctr));
+  return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ uint64_t eff_seed(const H16Args &a) {
+  return a.ctr ? a.seed ^ mix64(*a.ctr + 0x5851F42D4C957F2Dull) : a.seed;
+}
 
 __device__ __forceinline__ int lds_chunk(int row, int cl) { return cl ^ ((row >> 1) & 7); }
 
@@ -275,9 +299,12 @@ __device__ __forceinline__ void store_dl_tile(const H16Args &a, int m, int v, in
   }
 }
 
-template <int TS, bool BWD, int MC, int SEG = kMaxNT / TS>
+// SMP (forward only): draw the action instead of reading it (SAMPLE mode).
+template <int TS, bool BWD, int MC, int SEG = kMaxNT / TS, bool SMP = false>
 struct Hg16Epi {
+  static_assert(!(SMP && BWD), "sampling is a forward mode");
   static constexpr int S = SEG, NP = MC * S;  // S segments of TS tiles per column tile
+  uint64_t seed = 0;  // SMP: the launch seed (eff_seed), set by the kernel
   static constexpr int W32 = (16 * TS + 31) / 32;  // = ceil(A / 32) for every A with ceil(A / 16) = TS
   // The (mc, s) rows' mask words and actions are loaded one row ahead (and
   // the backward's per-sample gradients up front), so a row's compute runs
@@ -313,7 +340,7 @@ struct Hg16Epi {
       gen_[mc] = (BWD && a.g_ent) ? a.g_ent[mm] : 0.f;
     }
     load_mask_raw<W32>(a, row_of(a, 0, m0, v0, wid, c), mwn);
-    actn = a.action[row_of(a, 0, m0, v0, wid, c)];
+    actn = SMP ? -1 : a.action[row_of(a, 0, m0, v0, wid, c)];
   }
 
   __device__ __forceinline__ void row(const H16Args &a, f32x4 (&acc)[S * TS][MC], const int pi,
@@ -328,12 +355,26 @@ struct Hg16Epi {
     const int act = actn;
     if (pi + 1 < NP) {
       load_mask_raw<W32>(a, row_of(a, pi + 1, m0, v0, wid, c), mwn);
-      actn = a.action[row_of(a, pi + 1, m0, v0, wid, c)];
+      actn = SMP ? -1 : a.action[row_of(a, pi + 1, m0, v0, wid, c)];
     }
     mask_fix<W32>(a, mw);
     const int v = v0 + s;
     if (v >= a.V) return;  // workgroup-uniform: the last tile's missing segments
     const int64_t row = (int64_t)mm * a.V + v;
+    if (SMP && a.wait_ratio >= 0.f && a.bits) {
+      // PPOAgent.act's WAIT coin (ppo.py:151-156, vmp_policy.hip coin_flip):
+      // more than one invalid action and WAIT valid -> WAIT forbidden with
+      // probability 1 - wait_ratio, by the unfused head's per-row uniform
+      const int cnt = __popc(mw[0]) + __popc(mw[1]) + __popc(mw[2]) + __popc(mw[3]);
+      const int P = a.wait_index, pw = P >> 5;
+      const uint32_t pb = 1u << (P & 31);
+      const uint32_t wword = pw == 0 ? mw[0] : pw == 1 ? mw[1] : pw == 2 ? mw[2] : mw[3];
+      if (cnt > 1 && !(wword & pb) &&
+          uniform_at(seed ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) mw[i] |= i == pw ? pb : 0u;
+      }
+    }
     const int tgt = (act >= 0 && act < a.A) ? act : -1;
     // pass 1: masked logits (-1e7 at invalid actions, kPad past A) and the row max
     float xm[TS][4];
@@ -365,7 +406,7 @@ struct Hg16Epi {
         Ts = __builtin_fmaf(p[u][r], xm[u][r], Ts);
       }
     float xa = 0.f;
-    if (!BWD) {  // the given action's logit: tile u_t, register r_t of lane q_t
+    if (!BWD && !SMP) {  // the given action's logit: tile u_t, register r_t of lane q_t
       const int ut = tgt >> 4, rt = tgt & 3, qt = (tgt >> 2) & 3;
       float sel[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -380,7 +421,102 @@ struct Hg16Epi {
     const float lse = mx + logf(Ss);
     const float inv = 1.0f / Ss;
     const float H = lse - Ts * inv;  // Categorical.entropy, the tiled head's order
-    if (!BWD) {
+    if (!BWD && SMP) {
+      // inverse CDF over the row in action order j = 16 u + 4 q + r: the tile
+      // totals T[u] (same value on every lane), the tile u* holding target,
+      // then the first element of u* whose running sum passes target (the
+      // running sums of the lanes q are built in q order by every lane)
+      float tl[TS], T[TS];
+#pragma unroll
+      for (int u = 0; u < TS; u++) {
+        tl[u] = ((p[u][0] + p[u][1]) + p[u][2]) + p[u][3];
+        T[u] = xsum(tl[u]);
+      }
+      float tot = 0.f;
+#pragma unroll
+      for (int u = 0; u < TS; u++) tot += T[u];
+      const float target = uniform_at(seed, a.offset + (uint64_t)row) * tot;
+      int us = -1;
+      float base = 0.f, cum = 0.f;
+#pragma unroll
+      for (int u = 0; u < TS; u++) {
+        const float nx = cum + T[u];
+        if (us < 0 && nx > target) {
+          us = u;
+          base = cum;
+        }
+        cum = nx;
+      }
+      int ulast = 0;  // rounding: target past every sum -> the last tile with mass
+#pragma unroll
+      for (int u = 0; u < TS; u++) ulast = T[u] > 0.f ? u : ulast;
+      if (us < 0) {
+        us = ulast;
+        base = 0.f;
+#pragma unroll
+        for (int u = 0; u < TS; u++) base += u < ulast ? T[u] : 0.f;
+      }
+      float pu[4], xu[4], tu = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; r++) pu[r] = xu[r] = 0.f;
+#pragma unroll
+      for (int u = 0; u < TS; u++)
+        if (u == us) {
+          tu = tl[u];
+#pragma unroll
+          for (int r = 0; r < 4; r++) pu[r] = p[u][r], xu[r] = xm[u][r];
+        }
+      // the tile's lane sums in q order: lane q's running sum starts at
+      // base + t_0 + ... + t_{q-1}
+      const float t0 = __shfl(tu, c), t1 = __shfl(tu, 16 + c), t2 = __shfl(tu, 32 + c);
+      float pre = base;
+      pre = q > 0 ? pre + t0 : pre;
+      pre = q > 1 ? pre + t1 : pre;
+      pre = q > 2 ? pre + t2 : pre;
+      int pick = 0x7fffffff, lastpos = -1;
+      float cr = pre, xpick = 0.f, xlast = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        cr += pu[r];
+        const int j = 16 * us + 4 * q + r;
+        if (pick == 0x7fffffff && cr > target && pu[r] > 0.f) {
+          pick = j;
+          xpick = xu[r];
+        }
+        if (pu[r] > 0.f) {
+          lastpos = j;
+          xlast = xu[r];
+        }
+      }
+      // the smallest passing j over the 4 lanes of the sample (its logit
+      // travels with it); none (rounding inside the tile): the tile's last
+      // element with mass
+      int jb = pick;
+      float xb = xpick;
+#pragma unroll
+      for (int o = 16; o < 64; o <<= 1) {
+        const int jo = __shfl_xor(jb, o);
+        const float xo = __shfl_xor(xb, o);
+        if (jo < jb) jb = jo, xb = xo;
+      }
+      if (jb == 0x7fffffff) {
+        int jl = lastpos;
+        float xl = xlast;
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {
+          const int jo = __shfl_xor(jl, o);
+          const float xo = __shfl_xor(xl, o);
+          if (jo > jl) jl = jo, xl = xo;
+        }
+        jb = jl < 0 ? 0 : jl;
+        xb = xl;
+      }
+      if (live && q == 0) {
+        a.act_out[row] = jb;
+        a.row_lp[row] = xb - lse;
+        a.row_ent[row] = H;
+      }
+    } else if (!BWD) {
       xa = xsum(xa);  // one lane-element holds it, the others 0
       if (live && q == 0) {
         a.row_lp[row] = tgt >= 0 ? xa - lse : NAN;
@@ -470,7 +606,7 @@ __global__ void k_dsum(int64_t N, int G, const float *part, float *db) {
 
 // NW waves per workgroup, each owning MC = 16 / NW columns of 16 samples
 // (built: 8 waves x 2 columns, two waves per SIMD). Two LDS stages of BK = 64.
-template <int TS, bool BWD, int NW>
+template <int TS, bool BWD, int NW, bool SMP = false>
 __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
   constexpr int MC = 16 / NW, kThreads = 64 * NW;
@@ -562,7 +698,14 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
       for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
     continue;
 #endif
-    hg16_epilogue<TS, BWD, NW>(a, acc, m0, v0, wid, lane, colL);
+    {
+      Hg16Epi<TS, BWD, MC, S, SMP> ep;
+      if (SMP) ep.seed = eff_seed(a);
+      ep.begin(a, m0, v0, wid, lane);
+#pragma unroll
+      for (int pi = 0; pi < Hg16Epi<TS, BWD, MC, S, SMP>::NP; pi++)
+        ep.row(a, acc, pi, m0, v0, wid, lane, colL);
+    }
   }
   if (dsum) hg16_dsum_flush<TS, NW>(a, biasL + BNp, v0, g);
 }
@@ -1080,11 +1223,22 @@ int pick_groups(int n_tiles, int m_blocks) {
   return best;
 }
 
-template <bool BWD, int NW>
+template <bool BWD, int NW, bool SMP = false>
 hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
   const int64_t n_wg = a.team > 0 ? (int64_t)(a.teams + 7) / 8 * 8 * a.team
                                   : (int64_t)a.n_tiles * a.m_groups;
   const dim3 grid((unsigned)n_wg), block(64 * NW);
+  if (SMP) {  // sampling: the two-stage kernel only
+    switch (TS) {
+#define VMP_HG16S_CASE(T) \
+  case T: hipLaunchKernelGGL((k_hg16<T, false, NW, true>), grid, block, lds_bytes<T>(), st, a); break;
+      VMP_HG16S_CASE(1) VMP_HG16S_CASE(2) VMP_HG16S_CASE(3) VMP_HG16S_CASE(4)
+      VMP_HG16S_CASE(5) VMP_HG16S_CASE(6) VMP_HG16S_CASE(7)
+      default: hipLaunchKernelGGL((k_hg16<8, false, NW, true>), grid, block, lds_bytes<8>(), st, a); break;
+#undef VMP_HG16S_CASE
+    }
+    return hipGetLastError();
+  }
   // VMP_HG16_DEEP=1: the BK = 32 multi-stage kernel (measured slower: forward
   // 10.3 vs 9.06 ms, backward 14.8 vs 13.3 ms at NS 4 and 5, r04_hg16_deep.log)
   const char *dp = getenv("VMP_HG16_DEEP");
@@ -1174,10 +1328,10 @@ bool launch_res(H16Args &a, int TS, hipStream_t st, hipError_t &err) {
   return true;
 }
 
-template <bool BWD>
+template <bool BWD, bool SMP = false>
 hipError_t launch_hg16(H16Args &a, hipStream_t st) {
   const int TS = pick_ts(a.A);
-  {
+  if (!SMP) {
     hipError_t e;
     if (launch_res<BWD>(a, TS, st, e)) return e;
   }
@@ -1208,7 +1362,7 @@ hipError_t launch_hg16(H16Args &a, hipStream_t st) {
   } else {
     a.m_groups = pick_groups(a.n_tiles, a.m_blocks);
   }
-  return launch_ts<BWD, 8>(a, TS, st);
+  return launch_ts<BWD, 8, SMP>(a, TS, st);
 }
 
 int check_common(int32_t B, int32_t K, int32_t V, int32_t A, const void *h, const void *w,
@@ -1254,6 +1408,50 @@ extern "C" int vmp_actor_head_bf16_fwd(int32_t B, int32_t K, int32_t V, int32_t 
   a.h = h, a.w = weight, a.bias = bias, a.bits = mask_bits, a.action = action;
   a.row_lp = ws, a.row_ent = ws + rows;
   hipError_t e = launch_hg16<false>(a, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_rowsum, dim3((B + 3) / 4), dim3(256), 0, st, B, V, a.row_lp, a.row_ent,
+                       logprob, entropy);
+    e = hipGetLastError();
+  }
+  if (scratch) {
+    hipError_t f = hipFreeAsync(scratch, st);
+    if (e == hipSuccess) e = f;
+  }
+  if (e != hipSuccess) return policy_fail(VMP_EDEVICE, hipGetErrorString(e));
+  return VMP_OK;
+}
+
+extern "C" int vmp_actor_head_bf16_sample(int32_t B, int32_t K, int32_t V, int32_t A,
+                                          const uint16_t *h, const uint16_t *weight,
+                                          const float *bias, const uint32_t *mask_bits,
+                                          float wait_ratio, int32_t wait_index, uint64_t seed,
+                                          uint64_t offset, const uint64_t *rng_counter,
+                                          int32_t *action, float *logprob, float *entropy,
+                                          float *workspace, void *stream) {
+  int rc = check_common(B, K, V, A, h, weight, bias, mask_bits, action,
+                        "vmp_actor_head_bf16_sample: bad shape or null pointer");
+  if (rc) return rc;
+  if (!logprob || !entropy)
+    return policy_fail(VMP_EINVAL, "vmp_actor_head_bf16_sample: null output");
+  if (wait_ratio >= 0.f && (!mask_bits || wait_index < 0 || wait_index >= A))
+    return policy_fail(VMP_EINVAL, "vmp_actor_head_bf16_sample: the WAIT coin needs mask bits "
+                                   "and 0 <= wait_index < A");
+  if (B == 0) return VMP_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t rows = (int64_t)B * V;
+  float *scratch = nullptr, *ws = workspace;
+  if (!ws) {
+    hipError_t e = hipMallocAsync((void **)&scratch, 2 * rows * sizeof(float), st);
+    if (e != hipSuccess) return policy_fail(VMP_EOOM, hipGetErrorString(e));
+    ws = scratch;
+  }
+  H16Args a{};
+  a.B = B, a.K = K, a.V = V, a.A = A, a.W32 = (A + 31) / 32, a.ld = V * A;
+  a.h = h, a.w = weight, a.bias = bias, a.bits = mask_bits, a.act_out = action;
+  a.row_lp = ws, a.row_ent = ws + rows;
+  a.seed = seed, a.offset = offset, a.ctr = rng_counter;
+  a.wait_ratio = wait_ratio, a.wait_index = wait_index;
+  hipError_t e = launch_hg16<false, true>(a, st);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_rowsum, dim3((B + 3) / 4), dim3(256), 0, st, B, V, a.row_lp, a.row_ent,
                        logprob, entropy);

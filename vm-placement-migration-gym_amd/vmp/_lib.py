@@ -18,7 +18,8 @@ EXPORTS = (
     "vmp_heuristic_step", "vmp_rollout_heuristic", "vmp_mask", "vmp_mask_bool", "vmp_get_obs",
     "vmp_get_counters", "vmp_get_stats", "vmp_get_state", "vmp_get_rank", "vmp_gae",
     "vmp_policy_head", "vmp_policy_head_backward", "vmp_policy_head_backward_bf16",
-    "vmp_actor_head", "vmp_actor_head_bf16_fwd", "vmp_actor_head_bf16_bwd",
+    "vmp_actor_head", "vmp_actor_head_bf16_fwd", "vmp_actor_head_bf16_sample",
+    "vmp_actor_head_bf16_bwd",
     "vmp_actor_head_bf16_bwd_workspace", "vmp_record_enable",
     "vmp_record_read", "vmp_snapshot_bytes", "vmp_snapshot", "vmp_restore",
     "vmp_debug_fail_alloc", "vmp_debug_live_allocs", "vmp_debug_stamps", "vmp_debug_occupancy",
@@ -96,6 +97,8 @@ def lib():
         "vmp_actor_head": (ctypes.c_int, [i32, i32, i32, i32, i32, P, P, P, P, f32, i32, u64, u64,
                                            P, P, P, P, P, P, P]),
         "vmp_actor_head_bf16_fwd": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, P, P, P, P, P]),
+        "vmp_actor_head_bf16_sample": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, f32, i32,
+                                                       u64, u64, P, P, P, P, P, P]),
         "vmp_actor_head_bf16_bwd": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, P, P, P, P,
                                                     i32, P, P, P]),
         "vmp_actor_head_bf16_bwd_workspace": (ctypes.c_int64, [i32, i32, i32]),
@@ -117,7 +120,7 @@ def lib():
         if f is None:
             raise VmpError(f"libvmp lacks {name}")
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 9:
+    if L.vmp_abi_version() != 10:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

@@ -281,6 +281,31 @@ def actor_head_bf16_fwd(hb, wb, bias, V, A, bits, action):
     return act, lp, ent
 
 
+def actor_head_bf16_sample(hb, wb, bias, V, A, bits, rng: HeadRng, wait_ratio=-1.0,
+                           wait_index=-1):
+    """The bf16 rollout's draw (vmp_actor_head_bf16_sample): the actor's last
+    Linear on the bf16 matrix cores + the masked head in SAMPLE mode, with the
+    PPOAgent.act WAIT coin when wait_ratio >= 0 -> (action i32 [B, V], logprob
+    [B], entropy [B]); the logits never reach memory. The uniforms come from
+    `rng`'s counter-based stream as in policy_head."""
+    B = hb.shape[0] if hb.dim() == 2 else 0
+    dummy = torch.empty((B, V), dtype=torch.int32, device=hb.device)
+    B, K, _ = _bf16_operands(hb, wb, bias, V, A, bits, dummy, "actor_head_bf16_sample")
+    if wait_ratio >= 0 and (bits is None or not 0 <= wait_index < A):
+        raise ValueError("the WAIT coin needs mask bits and 0 <= wait_index < A")
+    seed, off = rng.take(B * V)
+    act = dummy
+    lp = torch.empty((B,), dtype=torch.float32, device=hb.device)
+    ent = torch.empty((B,), dtype=torch.float32, device=hb.device)
+    ws = torch.empty((2 * B * V,), dtype=torch.float32, device=hb.device)
+    check(lib().vmp_actor_head_bf16_sample(B, K, V, A, ptr(hb), ptr(wb), ptr(bias.contiguous()),
+                                           ptr(bits), float(wait_ratio), int(wait_index), seed,
+                                           off, ptr(rng.counter), ptr(act), ptr(lp), ptr(ent),
+                                           ptr(ws), _stream(hb)))
+    rng.advance()
+    return act, lp, ent
+
+
 def actor_head_bf16_bwd(hb, wb, bias, V, A, bits, action, g_lp, g_ent, out, dbias=None,
                         workspace=None):
     """The bf16 training backward (vmp_actor_head_bf16_bwd) over the rows of hb

@@ -334,9 +334,24 @@ class Network(nn.Module):
             act, lp, _ = H.actor_head(h, last.weight, last.bias, self.V, self.A, bits=bits,
                                       rng=self.rng, wait_ratio=wait_ratio, wait_index=wait_index)
             return act, lp
+        if self._bf16_sample(obs, bits):
+            # the bf16 leg's rollout: last Linear + head in SAMPLE mode on the
+            # matrix-core kernel the update's forward uses (no [B, V*A] logits)
+            last = self.actor[-1]
+            h = _run_mlp(self.actor[:-1], obs, self.precision).to(torch.bfloat16).contiguous()
+            act, lp, _ = H.actor_head_bf16_sample(h, _bf16_weight(last.weight), last.bias, self.V,
+                                                  self.A, bits, self.rng, wait_ratio, wait_index)
+            return act, lp
         act, lp, _ = self._head(self.actor_logits(obs), self.V, self.A, bits=bits, rng=self.rng,
                                 wait_ratio=wait_ratio, wait_index=wait_index)
         return act, lp
+
+    def _bf16_sample(self, obs, bits):
+        """Rollouts of the bf16 leg draw on the fused bf16 kernel where it
+        applies (VMP_BF16_SAMPLE=0: the logits path, for A/B measurement)."""
+        return (obs.is_cuda and self.bf16_fused()
+                and os.environ.get("VMP_BF16_SAMPLE", "1") != "0"
+                and (bits is None or (bits.is_contiguous() and bits.data_ptr() % 16 == 0)))
 
     def det(self, obs):
         """get_det_action's argmax (ppo.py:128-131) -> int32 [B, V]."""
