@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--chunk-gb", type=float, default=0.0, help="0: auto (1/8 of HBM)")
     ap.add_argument("--precision", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--lookahead", type=int, default=1, help="PPOConfig.kl_lookahead")
+    ap.add_argument("--dl-gb", type=float, default=0.0,
+                    help="PPOConfig.dlogits_chunk_bytes in GiB (0: the default)")
     args = ap.parse_args()
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
@@ -43,7 +45,9 @@ def main():
     ag = PPOAgent(env, PPOConfig(hidden_size=args.hidden, masked=True, batch_size=100,
                                  minibatch_size=25, migration_ratio=0.002,
                                  chunk_bytes=int(args.chunk_gb * (1 << 30)),
-                                 precision=args.precision, kl_lookahead=bool(args.lookahead)))
+                                 precision=args.precision, kl_lookahead=bool(args.lookahead),
+                                 **({"dlogits_chunk_bytes": int(args.dl_gb * (1 << 30))}
+                                    if args.dl_gb > 0 else {})))
     tr = ag.trainer()
     for _ in range(args.warmup):
         tr.collect()

@@ -67,7 +67,11 @@ class PPOConfig:
     value_loss_broadcast: bool = True  # ppo.py:266-270 [mb,1]-[mb] broadcast
     precision: str = "f32"             # "bf16": bf16 GEMM inputs, f32 accumulate/output
     chunk_bytes: int = 0               # logits budget per update chunk (0: from free HBM, fixed at the first update)
-    dlogits_chunk_bytes: int = 1 << 32  # bf16 fused head: dlogits rows per backward chunk
+    # bf16 fused head: dlogits bytes per backward chunk. 16 GiB holds a whole
+    # 204 800-row minibatch at V*A = 30 600 (12.5 GB): one dW / dh GEMM pair
+    # per minibatch instead of three, update 0.743 -> 0.718 s
+    # (profiles/r05_dlogits_chunk_ab.log); the peak grows by the same 8 GB
+    dlogits_chunk_bytes: int = 1 << 34
     kl_lookahead: bool = True          # step before the KL early-stop flag reaches the host,
                                        # roll back on a break (same accepted steps)
     seed_stride: int = 4               # env/episode reset seed spacing
@@ -382,7 +386,7 @@ class Network(nn.Module):
         head = 8 * self.V if self.bf16_fused() else 4 * self.V * self.A
         return head + 40 * H
 
-    def logprob_entropy(self, obs, bits, action, dlogits_chunk_bytes=1 << 32):
+    def logprob_entropy(self, obs, bits, action, dlogits_chunk_bytes=1 << 34):
         """get_action(obs, action, mask)'s logprob and entropy (ppo.py:115-126) for
         the update, differentiable. The bf16 leg with the HIP head runs the last
         Linear and the head as one node: fused on the bf16 matrix cores
