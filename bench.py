@@ -144,7 +144,7 @@ def main():
 
     # ---- fast-forward to steady state, phases staggered (untimed) ----
     reset_at, ff_total = fast_forward(env, "firstfit", seeds, args.ff_steps, args.phase_groups,
-                                      args.phase_delta, args.rollout_k)
+                                      args.phase_delta, args.rollout_k, offset=rank * N)
     torch.cuda.synchronize(dev)
 
     obs = torch.empty((N, D), dtype=torch.float32, device=dev)
@@ -357,14 +357,16 @@ def issue_roofline(pmc, N, kern_ms):
                       "GRBM_GUI_ACTIVE of the headline window)"}
 
 
-def fast_forward(env, policy, seeds, ff, groups, delta, k):
-    """Fused-rollout fast-forward with staggered phases: env i (group i mod
-    `groups`) is reset with its own seed at step (i mod groups) * delta, so after
-    ff + (groups - 1) * delta steps the envs' ages are spread over
-    (groups - 1) * delta steps. Returns (reset step per env, total steps)."""
+def fast_forward(env, policy, seeds, ff, groups, delta, k, offset=0):
+    """Fused-rollout fast-forward with staggered phases: env i (global index
+    offset + i, group (offset + i) mod `groups`) is reset with its own seed at
+    step group * delta, so after ff + (groups - 1) * delta steps the envs'
+    ages are spread over (groups - 1) * delta steps; an env's phase depends on
+    its global index only, so results do not depend on the rank count.
+    Returns (reset step per env, total steps)."""
     N = env.n_envs
     groups = max(1, int(groups))
-    grp = np.arange(N) % groups
+    grp = (int(offset) + np.arange(N)) % groups
     reset_at = grp * delta
     total = ff + (groups - 1) * delta
     events = [g * delta for g in range(1, groups)]
@@ -399,7 +401,7 @@ def bench_period(args, dev, rank, world, dist, cfg):
     G = max(1, args.period_groups)
     if G > 1:  # same window position, envs' ages spread as in the headline leg
         fast_forward(env, "firstfit", shard_seeds(rank, N), args.period_ff - (G - 1) * args.phase_delta,
-                     G, args.phase_delta, args.rollout_k)
+                     G, args.phase_delta, args.rollout_k, offset=rank * N)
     left = args.period_ff if G == 1 else 0
     while left > 0:
         env.rollout("firstfit", min(args.rollout_k, left))
@@ -469,7 +471,7 @@ def bench_nominal(args, dev, rank, world, dist):
     env = BatchedVmEnv(Config(**cfg), N, seeds=seeds, device=dev)
     env.eval(False)
     _, ff_total = fast_forward(env, "firstfit", seeds, 2000, args.phase_groups, args.phase_delta,
-                               args.rollout_k)
+                               args.rollout_k, offset=rank * N)
     L, h = _lib.lib(), env._bind()
     stream = torch.cuda.current_stream(dev)
     obs = torch.empty((N, 3 * V + 2 * P), dtype=torch.float32, device=dev)
@@ -653,7 +655,11 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
     torch.cuda.synchronize(dev)
     H = ag.config.hidden_size
     fused = precision == "bf16" and ag.model.bf16_fused()
-    runs = []  # per timed update: (collect s, update s, evaluated minibatches, minibatch steps, kl breaks)
+    # per timed update: (collect s, update s, evaluated minibatches, minibatch steps, kl
+    # breaks, executed minibatches). With the KL look-ahead a break also runs and
+    # discards the next minibatch (stats["rollbacks"] counts the broken one and
+    # that one): executed = steps + rollbacks >= evaluated = steps + breaks
+    runs = []
     for _ in range(max(1, int(args.ppo_updates))):
         if dist:
             dist.barrier()
@@ -667,7 +673,8 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
             dist.barrier()
         t2 = time.perf_counter()
         runs.append((_max_over_ranks(t1 - t0, dev, dist), _max_over_ranks(t2 - t1, dev, dist),
-                     st["minibatches"] + st["kl_breaks"], st["minibatches"], st["kl_breaks"]))
+                     st["minibatches"] + st["kl_breaks"], st["minibatches"], st["kl_breaks"],
+                     st["minibatches"] + max(st.get("rollbacks", 0), st["kl_breaks"])))
     col = np.array([r[0] for r in runs])
     upd = np.array([r[1] for r in runs])
     tot = col + upd
@@ -676,9 +683,12 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
     fus = np.array([ppo_update_flops(env.D, H, env.V * env.A, tr.T, N, r[2],
                                      ag.config.minibatch_size)[1] for r in runs])
     fc = ppo_update_flops(env.D, H, env.V * env.A, tr.T, N, 0, ag.config.minibatch_size)[0]
-    # the fused head's backward recomputes the last layer's logits: matrix-core
-    # work beyond the algorithmic count (what a PMC MFMA-busy pass sees)
-    recompute = np.array([r[2] * ag.config.minibatch_size * N * 2.0 * H * env.V * env.A
+    # executed: the look-ahead's discarded minibatches, and the fused head's
+    # backward recomputing the last layer's logits: matrix-core work beyond the
+    # algorithmic count (what a PMC MFMA-busy pass sees)
+    fex = np.array([ppo_update_flops(env.D, H, env.V * env.A, tr.T, N, r[5],
+                                     ag.config.minibatch_size)[1] for r in runs])
+    recompute = np.array([r[5] * ag.config.minibatch_size * N * 2.0 * H * env.V * env.A
                           for r in runs]) if fused else np.zeros(len(runs))
     med = int(np.argsort(upd)[len(upd) // 2])  # the median update
     upd_s, col_s, total = float(upd[med]), float(col[med]), float(np.median(tot))
@@ -688,7 +698,7 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
             "roofline": dict(mfma_roofline(float(fus[med]), upd_s, precision,
                                            "PPOAgent.update (all GEMMs, per GPU) / update wall "
                                            "time, median update"),
-                             executed_flops=float(fus[med] + recompute[med])),
+                             executed_flops=float(fex[med] + recompute[med])),
             "collect_roofline": mfma_roofline(fc, col_s, precision,
                                               "rollout actor forward / collect wall time"),
             "updates_timed": len(runs), "update_s_all": [float(x) for x in upd],
@@ -704,6 +714,7 @@ def bench_ppo_train(args, dev, rank, world, dist, precision="f32"):
             "s_per_update": total, "collect_s": float(np.median(col)),
             "update_s": float(np.median(upd)), "update_s_min": float(upd.min()),
             "minibatch_steps": [r[3] for r in runs], "kl_breaks": [r[4] for r in runs],
+            "minibatches_executed": [r[5] for r in runs],
             "parallelism": f"data-parallel x{world} (RCCL grad all-reduce)" if world > 1
             else "single GPU"}
 

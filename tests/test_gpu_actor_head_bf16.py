@@ -126,66 +126,44 @@ def test_fused_matches_logits_path_and_torch(B, K, V, A):
     assert _rel(gx_1, gx_f) < 1e-6 and _rel(gw_1, gw_f) < 1e-6 and _rel(gb_1, gb_f) < 1e-6
 
 
-@pytest.mark.parametrize("B,K,V,A", [(1500, 512, 300, 102), (700, 256, 13, 39),
-                                     (333, 64, 7, 22), (300, 128, 5, 128), (4096, 512, 30, 12)])
-def test_ping_pong_kernel_bit_exact(monkeypatch, B, K, V, A):
-    """VMP_HG16_PP=2 / 3 (two wave groups, epilogue beside the other group's
-    matrix loop; 2 / 3 LDS stages) against the two-stage kernel: the same MFMA chains, the same
-    epilogue code and the same per-wave bias-gradient sums in the same order,
-    so logprob, entropy, dlogits and db are bit-identical (ragged B: the last
-    half block is partial or empty)."""
+@pytest.mark.parametrize("B,K,V,A", [(25, 512, 31, 30), (25, 256, 31, 60), (25, 128, 33, 96),
+                                     (27, 64, 7, 22)])
+def test_mask_bits_row_views_any_alignment(B, K, V, A):
+    """the update hands the fused head row views of the mask bits
+    (bits[t0:t1] of a [T, N, V, W32] buffer), whose offset is a multiple of
+    W32 words only. With odd N*V and W32 = 1, 2, 3 the view is 4 / 8 / 12 B
+    past a 16-B boundary; the kernels need only the alignment of the vector
+    load they use, so forward, backward and SAMPLE mode run on such views
+    and equal the same bits copied to a fresh (aligned) buffer."""
     from vmp import head as H
-    h, w, b, mask, act = _case(B, K, V, A, seed=3 * B + V)
-    bits = H.pack_mask(mask, V, A)
-    hb, wb = h.bfloat16(), w.bfloat16()
-    g = torch.Generator().manual_seed(11)
+    h, w, b, mask, act = _case(B + 1, K, V, A, seed=17 * A + V)
+    full = H.pack_mask(mask, V, A)
+    view = full[1:]                       # one row of V * W32 words in
+    assert view.data_ptr() % 16 != 0
+    aligned = view.clone()
+    hb, wb = h[1:].bfloat16().contiguous(), w.bfloat16()
+    act = act[1:]
+    g = torch.Generator().manual_seed(5)
     glp = torch.randn(B, generator=g).to(DEV)
     gen = torch.randn(B, generator=g).to(DEV)
     outs = []
-    for pp in ("0", "2", "3"):
-        monkeypatch.setenv("VMP_HG16_PP", pp)
+    for bits in (view, aligned):
         _, lp, ent = H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act)
-        dl = torch.full((B, V * A), 7, dtype=torch.bfloat16, device=DEV)
+        dl = torch.zeros((B, V * A), dtype=torch.bfloat16, device=DEV)
         db = torch.zeros((V * A,), dtype=torch.float32, device=DEV)
         H.actor_head_bf16_bwd(hb, wb, b, V, A, bits, act, glp, gen, dl, dbias=db)
+        sa, slp, _ = H.actor_head_bf16_sample(hb, wb, b, V, A, bits, H.HeadRng(9), 0.5, A - 1)
         torch.cuda.synchronize()
-        outs.append((lp, ent, dl, db))
-    for o in outs[1:]:
-        for name, x, y in zip(("logprob", "entropy", "dlogits", "dbias"), outs[0], o):
-            assert torch.equal(torch.nan_to_num(x.float()), torch.nan_to_num(y.float())), name
-
-
-@pytest.mark.parametrize("B,K,V,A", [(1500, 512, 300, 102), (700, 256, 13, 39),
-                                     (333, 64, 7, 22), (300, 128, 5, 128), (4096, 512, 30, 12),
-                                     (2100, 512, 301, 101)])
-@pytest.mark.parametrize("rd", ["2", "4"])
-def test_resident_w_kernel_matches_two_stage(monkeypatch, B, K, V, A, rd):
-    """VMP_HG16_RES=1 (W slab resident in LDS, h straight into registers,
-    512-sample blocks) against the two-stage kernel: the same MFMA chain per
-    logit (K chunks in order) and the same epilogue, so logprob, entropy and
-    dlogits are bit-identical; the bias gradient sums the same f32 column
-    partials grouped by other blocks, so it agrees to f32 rounding (ragged B,
-    V not a multiple of the tile's segments, A = 128 and 101)."""
-    from vmp import head as H
-    h, w, b, mask, act = _case(B, K, V, A, seed=5 * B + V)
-    bits = H.pack_mask(mask, V, A)
-    hb, wb = h.bfloat16(), w.bfloat16()
-    g = torch.Generator().manual_seed(13)
-    glp = torch.randn(B, generator=g).to(DEV)
-    gen = torch.randn(B, generator=g).to(DEV)
-    monkeypatch.setenv("VMP_HG16_RD", rd)
-    outs = []
-    for res in ("0", "1"):
-        monkeypatch.setenv("VMP_HG16_RES", res)
-        _, lp, ent = H.actor_head_bf16_fwd(hb, wb, b, V, A, bits, act)
-        dl = torch.full((B, V * A), 7, dtype=torch.bfloat16, device=DEV)
-        db = torch.zeros((V * A,), dtype=torch.float32, device=DEV)
-        H.actor_head_bf16_bwd(hb, wb, b, V, A, bits, act, glp, gen, dl, dbias=db)
-        torch.cuda.synchronize()
-        outs.append((lp, ent, dl, db))
-    for name, x, y in zip(("logprob", "entropy", "dlogits"), outs[0][:3], outs[1][:3]):
+        outs.append((lp, ent, dl, db, sa, slp))
+    for name, x, y in zip(("logprob", "entropy", "dlogits", "dbias", "sample", "sample_lp"),
+                          *outs):
         assert torch.equal(torch.nan_to_num(x.float()), torch.nan_to_num(y.float())), name
-    torch.testing.assert_close(outs[1][3], outs[0][3], rtol=1e-5, atol=1e-6 * B)
+    # a misaligned base for the row's vector load is still refused loudly
+    if (A + 31) // 32 in (2, 4):
+        raw = torch.zeros(full.numel() + 1, dtype=torch.int32, device=DEV)
+        bad = raw[1:].view(full.shape)[1:]
+        with pytest.raises(ValueError, match="misaligned"):
+            H.actor_head_bf16_fwd(hb, wb, b, V, A, bad, act)
 
 
 @pytest.mark.parametrize("B,K,V,A", [(1500, 512, 300, 102), (700, 256, 13, 39),

@@ -26,6 +26,11 @@ def _need_gpu():
         pytest.fail("gpu tests need a HIP device")
 
 
+CFG100 = dict(pms=100, vms=300, service_length=1000, arrival_rate=1.8182, training_steps=10000,
+              eval_steps=100000, seed=0, reward_function="wr", sequence="uniform",
+              cap_target_util=True, beta=0.5, allow_null_action=True)
+
+
 def _g(name):
     return np.load(os.path.join(GOLDEN, name))
 
@@ -370,4 +375,69 @@ def test_bf16_graph_reads_the_live_parameters():
         assert not torch.equal(expect, expect_old), "the update should change some actions"
         g.replay()
         assert torch.equal(g.actions, expect), how
+    env.close()
+
+
+def _change_rel_cos(sd, d, pre):
+    """(relative L2 of sd - reference over the reference's change, cosine of
+    the two parameter changes) over every parameter."""
+    keys = sorted(sd)
+    ours = np.concatenate([(sd[k] - d["p0_" + k]).ravel() for k in keys]).astype(np.float64)
+    ref = np.concatenate([(d[pre + k] - d["p0_" + k]).ravel() for k in keys]).astype(np.float64)
+    rel = float(np.linalg.norm(ours - ref) / np.linalg.norm(ref))
+    return rel, float(ours @ ref / np.linalg.norm(ours) / np.linalg.norm(ref))
+
+
+def test_bf16_update_vs_reference_update_10yml():
+    """the bf16 training leg (precision="bf16": bf16 GEMM
+    inputs, f32 accumulate, the fused matrix-core actor head at hidden 64)
+    against the reference's f32 update() on its recorded batch
+    (tests/golden/ppo_update.npz, src/agents/ppo.py:229-295): the same 16
+    minibatch steps and no KL break, the parameter change within 3e-2 relative
+    L2 of the reference's and pointing the same way (cosine >= 0.999). Bound:
+    bf16 keeps 8 significand bits, and AdamW's first steps move every element
+    by ~lr whatever its gradient's size, so rounding that flips a near-zero
+    gradient element moves that element the other way; a CPU emulation of the
+    same bf16 GEMM rounding with the torch head gives 1.2e-2 / 0.99993."""
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import PPOAgent, PPOConfig
+    d = _g("ppo_update.npz")
+    env = BatchedVmEnv(Config(**CFG10), 1, device=DEV)
+    ag = PPOAgent(env, PPOConfig(hidden_size=64, episodes=1, precision="bf16"))
+    assert ag.model.bf16_fused()  # the fused head kernels run this update
+    ag.model.load_state_dict({k[3:]: torch.tensor(d[k]) for k in d.files if k.startswith("p0_")})
+    st = ag.update(*[torch.tensor(d[k]) for k in ("b_mask", "b_action", "b_obs", "b_next_obs",
+                                                    "b_logprob", "b_reward", "b_done")])
+    assert st["minibatches"] == 16 and st["kl_breaks"] == 0
+    sd = {k: v.detach().cpu().numpy() for k, v in ag.model.state_dict().items()}
+    rel, cos = _change_rel_cos(sd, d, "p1_")
+    print(f"bf16 update vs reference (10.yml, hidden 64): rel L2 {rel:.3e}, cos {cos:.6f}")
+    assert rel <= 3e-2 and cos >= 0.999, (rel, cos)
+    env.close()
+
+
+@pytest.mark.parametrize("k_epochs", [2, 4])
+def test_bf16_update_vs_reference_update_100yml(k_epochs):
+    """The bf16 leg at the 100.yml shape (V 300, A 102, D 1100) against the
+    reference's update on its own sampled batch (tests/golden/ppo100_update.npz,
+    hidden 8: the bf16 logits path, BF16ActorHead): the reference's minibatch /
+    KL-break sequence (2 epochs: 8 steps; 4 epochs: 14 steps and the epoch-4
+    break) and the parameter change within 0.15 relative L2 (cosine >= 0.99).
+    Bound: the 1 100-wide first layer sees bf16-rounded observations; CPU
+    emulation of the rounding measures 0.103 / 0.093 (cosine 0.995 / 0.996)."""
+    from tests.test_ppo_cpu import _ppo100_update
+    from vmp.batched import BatchedVmEnv
+    from vmp.config import Config
+    from vmp.ppo import PPOAgent, PPOConfig
+    env = BatchedVmEnv(Config(**CFG100), 1, device=DEV)
+    ag = PPOAgent(env, PPOConfig(hidden_size=8, episodes=1, batch_size=100, minibatch_size=25,
+                                 migration_ratio=0.002, k_epochs=k_epochs, precision="bf16"))
+    d, ag, st = _ppo100_update(k_epochs, agent=ag)
+    calls = d[("e2_" if k_epochs == 2 else "") + "ref_calls"]
+    assert st["minibatches"] == calls[1] and st["minibatches"] + st["kl_breaks"] == calls[0]
+    sd = {k: v.detach().cpu().numpy() for k, v in ag.model.state_dict().items()}
+    rel, cos = _change_rel_cos(sd, d, "p1_e2_" if k_epochs == 2 else "p1_")
+    print(f"bf16 update vs reference (100.yml, {k_epochs} epochs): rel L2 {rel:.3e}, cos {cos:.6f}")
+    assert rel <= 0.15 and cos >= 0.99, (rel, cos)
     env.close()

@@ -61,14 +61,12 @@ constexpr int kMaxNT = 14;     // 16-column accumulator tiles per workgroup
 constexpr float kMasked = -1e7f;   // ppo.py:119
 constexpr float kPad = -1e30f;     // tile columns past A: p = 0, never the max
 constexpr float kLog2e = 1.44269504088896341f;
-#ifndef VMP_HG16_PIPE
-#define VMP_HG16_PIPE 4  // W fragments in flight ahead of their MFMAs
-#endif
+constexpr int kPipe = 4;       // W fragments in flight ahead of their MFMAs
+constexpr int kTeam = 8;       // XCD team size (hg16_tile)
 
 struct H16Args {
   int B, K, V, A, W32, n_tiles, m_blocks, m_groups, ld;
   int team, teams;  // XCD teams (launch_hg16); team 0: one column tile per block index
-  int stag;         // resident-W kernel: block-walk stagger (hg16r walk)
   const uint16_t *h, *w;
   const float *bias;
   const uint32_t *bits;
@@ -112,20 +110,8 @@ __device__ __forceinline__ bf16x8 frag(const char LDSP *base, int row, int cl) {
 // global -> LDS staging of one K stage: W rows (tile columns, segment-padded)
 // then h rows, 8 rows of 128 B per wave instruction; lane L writes LDS
 // position L % 8 of row L / 8 with the logical chunk that position holds.
-// One global_load_lds_dwordx4 in inline asm: the compiler does not see an
-// LDS DMA, so it inserts no vmcnt wait of its own for it (the ping-pong
-// kernel's register reuse made it wait for the whole stage before the first
-// MFMA). The caller counts these in its own s_waitcnt vmcnt. M0 (the wave's
-// LDS destination) is written here only; no other code of the kernels that
-// use it reads M0.
-__device__ __forceinline__ void glds16_asm(const void *src, char LDSP *dst) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
-               : "memory");
-}
-
-// NW issuing waves (wid < NW), BM h rows; ASM: glds16_asm instead of the builtin.
-template <int TS, int NT, int NW, int BM = kBM, bool ASM = false>
+// NW issuing waves (wid < NW), BM h rows.
+template <int TS, int NT, int NW, int BM = kBM>
 __device__ __forceinline__ void stage_issue(const H16Args &a, char LDSP *buf, int v0, int m0,
                                             int k0, int wid, int lane) {
   constexpr int SA = 16 * TS, BNp = 16 * NT, PW = BNp / 8, PIECES = (BNp + BM) / 8;
@@ -148,8 +134,7 @@ __device__ __forceinline__ void stage_issue(const H16Args &a, char LDSP *buf, in
       }
       src += k0 + 8 * lds_chunk(r, p);
       char LDSP *dst = buf + (i < PW ? 0 : BNp * kRow) + (r - rl) * kRow;
-      if (ASM) glds16_asm(src, dst);
-      else __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)dst, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)dst, 16, 0, 0);
     }
   }
 }
@@ -217,7 +202,7 @@ __device__ __forceinline__ void load_mask(const H16Args &a, int64_t row, uint32_
 // of one XCD take the same column tile (its W tile stays in that XCD's L2
 // while they walk M blocks j, j + G, ...) and the 32 / team teams resident on
 // an XCD walk the same M blocks (h tiles shared): at team 8, an L2 working set
-// of 4 W tiles + 8 h tiles instead of 32 W tiles (VMP_HG16_TEAM: 0 / 2 / 4 / 8
+// of 4 W tiles + 8 h tiles instead of 32 W tiles (kTeam; 0 / 2 / 4 / 8
 // measured, profiles/r04_hg16_team.log). False: a padding block.
 __device__ __forceinline__ bool hg16_tile(const H16Args &a, int &n_tile, int &g) {
   if (a.team > 0) {
@@ -279,16 +264,9 @@ __device__ __forceinline__ void store_dl_tile(const H16Args &a, int m, int v, in
   if (((a.A | a.ld) & 1) == 0) {
     // inner tiles hold only real columns (TS = ceil(A / 16)); in the last
     // one j0 is a multiple of 4, so a lane's valid columns are 0, 2 or 4
-#ifdef VMP_HG16_OLDST  // A/B: two dword stores per tile
-    if (live && (u < TS - 1 || j0 + 2 < a.A)) {
-      *reinterpret_cast<uint32_t *>(dst) = pk0;
-      *reinterpret_cast<uint32_t *>(dst + 2) = pk1;
-    } else if (live && j0 < a.A) {
-#else
     if (live && (u < TS - 1 || j0 + 2 < a.A)) {
       *reinterpret_cast<u32x2u *>(dst) = u32x2u{pk0, pk1};
     } else if (live && j0 < a.A) {
-#endif
       *reinterpret_cast<uint32_t *>(dst) = pk0;
     }
   } else if (live && j0 < a.A) {
@@ -557,25 +535,11 @@ struct Hg16Epi {
                              ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
         const uint32_t pk1 = (uint32_t)__builtin_bit_cast(uint16_t, b2) |
                              ((uint32_t)__builtin_bit_cast(uint16_t, b3) << 16);
-#ifdef VMP_HG16_NO_STORE  // timing-only build: no dlogits stores (outputs wrong)
-        asm volatile("" ::"v"(pk0), "v"(pk1));
-        continue;
-#endif
         store_dl_tile<TS>(a, m, v, u, q, pk0, pk1);
       }
     }
   }
 };
-
-template <int TS, bool BWD, int NW>
-__device__ __forceinline__ void hg16_epilogue(const H16Args &a,
-                                              f32x4 (&acc)[kMaxNT / TS * TS][16 / NW], int m0,
-                                              int v0, int wid, int lane, float LDSP *colL) {
-  Hg16Epi<TS, BWD, 16 / NW> ep;
-  ep.begin(a, m0, v0, wid, lane);
-#pragma unroll
-  for (int pi = 0; pi < Hg16Epi<TS, BWD, 16 / NW>::NP; pi++) ep.row(a, acc, pi, m0, v0, wid, lane, colL);
-}
 
 // The workgroup's bias-gradient partial: its waves' LDS column sums added in
 // wave order and stored to a.dpart[g][v A + j] (one workgroup per (column
@@ -664,7 +628,7 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
       // before its use, every pair waited on it); both K halves' h fragments
       // up front. The sched_group_barriers pin the pattern
       // {MFMA, MFMA, ds_read} so the compiler does not sink the reads again.
-      constexpr int kPipe = VMP_HG16_PIPE, NF = 2 * NT;
+      constexpr int NF = 2 * NT;
       bf16x8 hf[2][MC];
 #pragma unroll
       for (int kk = 0; kk < 2; kk++)
@@ -691,13 +655,6 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
       __syncthreads();
     }
     sb = (sb + nk) & 1;
-#ifdef VMP_HG16_GEMM_ONLY  // timing-only build: the main loop alone (outputs wrong)
-#pragma unroll
-    for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-      for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
-    continue;
-#endif
     {
       Hg16Epi<TS, BWD, MC, S, SMP> ep;
       if (SMP) ep.seed = eff_seed(a);
@@ -710,498 +667,12 @@ __global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16(H16Args a) {
   if (dsum) hg16_dsum_flush<TS, NW>(a, biasL + BNp, v0, g);
 }
 
-// ---- the ping-pong kernel: two wave groups, one in the matrix loop while
-// the other runs its epilogue ----
-// The two-stage kernel's epilogue (a third of the forward, half of the
-// backward) runs on all 8 waves at once, so the matrix pipes idle through it.
-// Here the workgroup's M blocks are cut into halves of kHB = 128 samples;
-// group G (waves 4G..4G+3, one per SIMD) computes half blocks hb = G, G + 2,
-// ... and the groups are one half block apart in time: in the K steps of half
-// block hb (group hb & 1, the "main" group, MFMAs from LDS), the other group
-// runs the epilogue of half block hb - 1 out of its accumulators, its rows
-// spread over those K steps. Each SIMD then pairs one matrix wave with one
-// VALU wave (MI355X_MICROARCH.md "Two waves per SIMD": complementary segments
-// are what overlap). The main group stages the next K step (its own next, or
-// the other group's first) into the stage it does not read; it waits for its
-// own DMA before the step's barrier, the epilogue group waits for nothing
-// (its mask loads and dlogits stores stay in flight across barriers): raw
-// s_barrier, not __syncthreads, whose fence would drain them.
-constexpr int kHB = 128;  // samples per half block (4 waves x 2 columns of 16)
-#ifndef VMP_HG16P_ASM
-#define VMP_HG16P_ASM true  // the stage DMA through glds16_asm
-#endif
-
-//
-// NS LDS stages (2 or 3). At 3 the main group issues K step p + 2 in step p,
-// so a stage has two steps to land: in step p the main group waits for step
-// p + 1's pieces (its own from step p - 1; vmcnt(PW) leaves this step's PW
-// in flight) except in a half block's first step, where step p + 1 came from
-// the other group - which waits for it (vmcnt(0)) in its first epilogue step.
-template <int TS, bool BWD, int NS>
-__global__ __launch_bounds__(512, 2) void k_hg16p(H16Args a) {
-  constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
-  constexpr int MC = 2, kThreads = 512;
-  constexpr int kStageW = BNp * kRow, kStage = kStageW + kHB * kRow;
-  constexpr int PW = (BNp + kHB) / 8 / 4;  // pieces per main wave per stage
-  static_assert(((BNp + kHB) / 8) % 4 == 0, "stage pieces split evenly over 4 waves");
-  static_assert(NS == 2 || NS == 3, "2 or 3 stages");
-  using Epi = Hg16Epi<TS, BWD, MC>;
-  constexpr int NP = Epi::NP;
-  extern __shared__ __align__(16) char lds_raw[];
-  char LDSP *lds = (char LDSP *)lds_raw;
-  float LDSP *biasL = reinterpret_cast<float LDSP *>(lds + NS * kStage);
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int grp = wid >> 2, wg = wid & 3;  // group, wave in group
-  const int q = lane >> 4, c = lane & 15;
-  int n_tile, g;
-  if (!hg16_tile(a, n_tile, g)) return;
-  const int v0 = n_tile * S;
-  const bool dsum = BWD && a.dpart;
-  float LDSP *colL = dsum ? biasL + BNp + wid * BNp : nullptr;
-  for (int n = t; n < BNp; n += kThreads) {
-    const int s = n / SA, j = n - s * SA, v = v0 + s;
-    biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
-  }
-  if (dsum)
-    for (int n = t; n < 8 * BNp; n += kThreads) biasL[BNp + n] = 0.f;
-  const int nk = a.K / kBK;
-  const int nblk = (a.m_blocks - g + a.m_groups - 1) / a.m_groups;
-  const int nhb = 2 * nblk, nst = nhb * nk;  // half blocks, K steps of all of them
-  auto half_m0 = [&](int hb) { return (g + (hb >> 1) * a.m_groups) * kBM + (hb & 1) * kHB; };
-  // global step st = K step st % nk of half block st / nk, in stage st % NS
-  auto issue4 = [&](int st) {
-    const int h = st / nk;
-    stage_issue<TS, NT, 4, kHB, VMP_HG16P_ASM>(a, lds + (st % NS) * kStage, v0, half_m0(h),
-                                               (st - h * nk) * kBK, wg, lane);
-  };
-  // the first NS - 1 steps, by all 8 waves
-#pragma unroll
-  for (int st = 0; st < NS - 1; st++) {
-    if (st < nst) {
-      const int h = st / nk;
-      stage_issue<TS, NT, 8, kHB, VMP_HG16P_ASM>(a, lds + st * kStage, v0, half_m0(h),
-                                                 (st - h * nk) * kBK, wid, lane);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  f32x4 acc[NT][MC];
-  Epi ep;
-  int hb = 0, k = 0;  // phase p = hb nk + k: K step k of half block hb
-#pragma unroll 1
-  for (int p = 0; p < nst + nk; p++) {
-    if (hb < nhb && (hb & 1) == grp) {
-      // ---- main: K step k of half block hb ----
-      if (k == 0) {
-#pragma unroll
-        for (int nt = 0; nt < NT; nt++) {
-          const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
-#pragma unroll
-          for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
-        }
-      }
-      const char LDSP *cur = lds + (p % NS) * kStage;
-      const bool issued = p + NS - 1 < nst;
-      if (issued) issue4(p + NS - 1);
-      const char LDSP *Hs = cur + kStageW;
-      constexpr int kPipe = VMP_HG16_PIPE, NF = 2 * NT;
-      bf16x8 hf[2][MC];
-#pragma unroll
-      for (int kk = 0; kk < 2; kk++)
-#pragma unroll
-        for (int mc = 0; mc < MC; mc++) hf[kk][mc] = frag(Hs, 16 * (MC * wg + mc) + c, 4 * kk + q);
-      bf16x8 wf[kPipe];
-#pragma unroll
-      for (int i = 0; i < kPipe; i++) wf[i] = frag(cur, 16 * (i % NT) + c, 4 * (i / NT) + q);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * MC + kPipe, 0);
-#pragma unroll
-      for (int i = 0; i < NF; i++) {
-        const int kk = i / NT, nt = i % NT;
-#pragma unroll
-        for (int mc = 0; mc < MC; mc++)
-          acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i % kPipe], hf[kk][mc], acc[nt][mc], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, MC, 0);
-        if (i + kPipe < NF) {
-          const int j = i + kPipe;
-          wf[i % kPipe] = frag(cur, 16 * (j % NT) + c, 4 * (j / NT) + q);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-      }
-      if (NS == 2) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // The epilogue's cross-step loads (row prefetches, per-sample
-        // gradients) are dead here, but the compiler's wait analysis cannot
-        // see that this step never follows one of them with the load still in
-        // flight: had their registers been reused above, it would wait on
-        // vmcnt before that write - behind this step's stage DMA. Kept live
-        // (and read) only here, after the step's own wait, they are not reused.
-        ep.keep_live();
-      } else if (k > 0) {
-        if (issued) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else if (hb >= 1 && ((hb - 1) & 1) == grp) {
-      // NS = 3, the first epilogue step: the next step's stage is ours
-      if (NS == 3 && k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // ---- epilogue of half block hb - 1: rows [k NP / nk, (k + 1) NP / nk) ----
-      const int m0 = half_m0(hb - 1);
-#ifndef VMP_HG16_GEMM_ONLY
-      if (k == 0) ep.begin(a, m0, v0, wg, lane);
-      const int r0 = k * NP / nk, r1 = (k + 1) * NP / nk;
-#pragma unroll
-      for (int pi = 0; pi < NP; pi++)
-        if (pi >= r0 && pi < r1) ep.row(a, acc, pi, m0, v0, wg, lane, colL);
-#else
-      if (k == 0)
-#pragma unroll
-        for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-          for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
-#endif
-    }
-    // the stage read in this step may be overwritten from the next; the next
-    // step's stage has landed (the main group's vmcnt(0) above)
-    __builtin_amdgcn_s_barrier();
-    if (++k == nk) k = 0, hb++;
-  }
-  if (dsum) hg16_dsum_flush<TS, 8>(a, biasL + BNp, v0, g);
-}
-
-// ---- the resident-W kernel ----
-// The two-stage kernel stages W and h through LDS every K step: 60 LDS-DMA
-// pieces per step and workgroup, each holding its wave's issue for 100+
-// cycles (MI355X_MICROARCH.md, LDS-DMA piece issue cost), plus a barrier per
-// step - together they cap its matrix loop at ~45 % of the bf16 peak. Here a
-// workgroup's column tile is at most 128 columns (S = 8 / TS whole segments),
-// so its whole W slab (128 x K bf16, 128 KB at K = 512) is loaded into LDS
-// once and stays resident while the workgroup walks its M blocks; the h
-// operand, private to each wave (wave w owns samples 64 w .. 64 w + 63 of a
-// 512-sample block), is read from global memory straight into the MFMA
-// B-operand registers, RD K chunks of 32 ahead. The matrix loop has no
-// barrier and no DMA, so the 8 waves run free: one wave's epilogue (VALU,
-// dlogits stores) overlaps its SIMD partner's MFMAs.
-// W rows are 2K bytes; 16-B chunk c of row r sits at chunk c ^ (r & SW) (SW
-// 15, or 7 at K = 64): the ds_read_b128 fragment groups hit 16 distinct bank
-// quads. XCD-aware walk (hg16r_tile): the workgroups resident on one XCD take
-// different column tiles and the same M group, so each h block is read from
-// HBM about once per XCD and from L2 by the others.
-constexpr int kRBM = 512;  // samples per M block (8 waves x 4 columns of 16)
-constexpr int kRMC = 4;    // 16-sample columns per wave
-
-template <int TS>
-constexpr int res_seg() { return 8 / TS; }  // segments per column tile
-
-// the workgroup's column tile and M group (false: a padding workgroup)
-__device__ __forceinline__ bool hg16r_tile(const H16Args &a, int &n_tile, int &g) {
-  const int b = blockIdx.x, xcd = b & 7, i = b >> 3;
-  n_tile = i % a.n_tiles;
-  g = (i / a.n_tiles) * 8 + xcd;
-  return g < a.m_groups && g < a.m_blocks;
-}
-
-template <int TS, bool BWD, int RD>
-__global__ __launch_bounds__(512, 2) void k_hg16r(H16Args a) {
-  constexpr int S = res_seg<TS>(), NT = S * TS, SA = 16 * TS, BN = 16 * NT, MC = kRMC;
-  using Epi = Hg16Epi<TS, BWD, MC, S>;
-  extern __shared__ __align__(16) char lds_raw[];
-  char LDSP *Wl = (char LDSP *)lds_raw;
-  const int K = a.K, rowb = 2 * K;
-  float LDSP *biasL = reinterpret_cast<float LDSP *>(Wl + (size_t)BN * rowb);
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int q = lane >> 4, c = lane & 15;
-  int n_tile, g;
-  if (!hg16r_tile(a, n_tile, g)) return;
-  const int v0 = n_tile * S;
-  const bool dsum = BWD && a.dpart;
-  float LDSP *colL = dsum ? biasL + BN + wid * BN : nullptr;
-  const int sw = K >= 128 ? 15 : 7;
-  // ---- W slab -> LDS, once: piece p = LDS bytes [1 KB p, 1 KB (p + 1)) ----
-  {
-    const int pieces = BN * rowb / 1024;
-    for (int p = wid; p < pieces; p += 8) {
-      const int pos = p * 1024 + 16 * lane;
-      const int r = pos / rowb, pc = (pos - r * rowb) >> 4;
-      const int sg = r / SA, j = r - sg * SA, v = v0 + sg;
-      const int wr = (v < a.V && j < a.A) ? v * a.A + j : v0 * a.A;  // pad rows: any row
-      const uint16_t *src = a.w + (int64_t)wr * K + 8 * (pc ^ (r & sw));
-      __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)(Wl + p * 1024), 16, 0, 0);
-    }
-  }
-  for (int n = t; n < BN; n += 512) {
-    const int sg = n / SA, j = n - sg * SA, v = v0 + sg;
-    biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
-  }
-  if (dsum)
-    for (int n = t; n < 8 * BN; n += 512) biasL[BN + n] = 0.f;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  const int nkc = K / 32;  // K chunks of one MFMA each
-  // this lane's W fragment offsets (row 16 nt + c, logical chunk 4 kc + q)
-  const int wrow = c * rowb;
-  // the walk: blocks g + G t, t = 0 .. nblk - 1, started at t0 = (n_tile %
-  // stag) nblk / stag and wrapped, so the XCD's workgroups (consecutive
-  // column tiles, one M group) are spread over stag blocks: a block's h
-  // chunks miss in L2 for the first group to reach it only, instead of for
-  // all 32 workgroups at once (lockstep walks wait on the same misses)
-  const int nblk = (a.m_blocks - g + a.m_groups - 1) / a.m_groups;
-  const int t0 = a.stag > 1 ? (n_tile % a.stag) * nblk / a.stag : 0;
-#pragma unroll 1
-  for (int tt = 0; tt < nblk; tt++) {
-    const int t = tt + t0 < nblk ? tt + t0 : tt + t0 - nblk;
-    const int mb = g + t * a.m_groups;
-    const int m0 = mb * kRBM;
-    const uint16_t *hp[MC];
-#pragma unroll
-    for (int mc = 0; mc < MC; mc++) {
-      const int m = m0 + 16 * (MC * wid + mc) + c;
-      hp[mc] = a.h + (int64_t)(m < a.B ? m : a.B - 1) * K + 8 * q;
-    }
-    f32x4 acc[NT][MC];
-#pragma unroll
-    for (int nt = 0; nt < NT; nt++) {
-      const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
-#pragma unroll
-      for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
-    }
-    bf16x8 hr[RD][MC];  // h fragments of K chunks kc .. kc + RD - 1
-#pragma unroll
-    for (int d = 0; d < RD - 1; d++)
-#pragma unroll
-      for (int mc = 0; mc < MC; mc++) hr[d][mc] = *reinterpret_cast<const bf16x8 *>(hp[mc] + 32 * d);
-    // W fragments run kPipe ahead of their MFMAs in the flattened (chunk,
-    // tile) order, across the RD-chunk loop's back edge too; the
-    // sched_group_barriers pin {MC MFMAs, one ds_read} so the reads are not
-    // sunk to their use (one read ahead, each read's latency was exposed)
-    constexpr int NF = RD * NT, kPipe = NF % 4 == 0 ? 4 : 2;
-    static_assert(NF % kPipe == 0, "the W pipeline rotates with the loop");
-    auto wfrag = [&](int kc, int nt) {
-      return *reinterpret_cast<const bf16x8 LDSP *>(Wl + wrow + 16 * nt * rowb +
-                                                    (((4 * kc + q) ^ (c & sw)) << 4));
-    };
-    bf16x8 wf[kPipe];
-#pragma unroll
-    for (int i = 0; i < kPipe; i++) wf[i] = wfrag(i / NT, i % NT);
-#pragma unroll 1
-    for (int kc0 = 0; kc0 < nkc; kc0 += RD) {
-      const bool more = kc0 + RD < nkc;
-#pragma unroll
-      for (int i = 0; i < NF; i++) {
-        const int d = i / NT, nt = i % NT;
-        if (nt == 0 && kc0 + d + RD - 1 < nkc) {
-          // chunk kc + RD - 1 into the slot chunk kc - 1 used
-#pragma unroll
-          for (int mc = 0; mc < MC; mc++)
-            hr[(d + RD - 1) % RD][mc] =
-                *reinterpret_cast<const bf16x8 *>(hp[mc] + 32 * (kc0 + d + RD - 1));
-        }
-#pragma unroll
-        for (int mc = 0; mc < MC; mc++)
-          acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i % kPipe], hr[d][mc], acc[nt][mc], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, MC, 0);
-        const int j = i + kPipe;
-        if (j < NF) {
-          wf[i % kPipe] = wfrag(kc0 + j / NT, j % NT);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        } else if (more) {
-          wf[i % kPipe] = wfrag(kc0 + RD + (j - NF) / NT, (j - NF) % NT);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-      }
-    }
-#ifdef VMP_HG16_GEMM_ONLY
-#pragma unroll
-    for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-      for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
-#else
-    Epi ep;
-    ep.begin(a, m0, v0, wid, lane);
-#pragma unroll
-    for (int pi = 0; pi < Epi::NP; pi++) ep.row(a, acc, pi, m0, v0, wid, lane, colL);
-#endif
-  }
-  if (dsum) {  // the workgroup's bias-gradient partial, waves in order
-    __syncthreads();
-    for (int n = t; n < BN; n += 512) {
-      const int sg = n / SA, j = n - sg * SA, v = v0 + sg;
-      float x = 0.f;
-#pragma unroll
-      for (int w = 0; w < 8; w++) x += biasL[BN + w * BN + n];
-      if (v < a.V && j < a.A) a.dpart[(int64_t)g * a.V * a.A + v * a.A + j] = x;
-    }
-  }
-}
-
-template <int TS>
-constexpr size_t res_lds_fixed() {  // bytes besides the W slab: bias + 8 waves' column sums
-  return 9 * 16 * (res_seg<TS>() * TS) * sizeof(float);
-}
-template <int TS>
-size_t res_lds_bytes(int K) { return (size_t)16 * res_seg<TS>() * TS * 2 * K + res_lds_fixed<TS>(); }
-
-// ---- the deep-pipeline kernel: BK = 32 (64-B rows), NS LDS stages ----
-// One stage is (BNp + BM) rows x 64 B (30 KB at NT = 14), so NS - 1 stages are
-// in flight while one is consumed (the two-stage kernel above has one: its
-// 61 KB stages fill LDS at two). The K steps of all the workgroup's M blocks
-// form one sequence, so the next block's first stages load under this block's
-// last MFMAs and its epilogue.
-constexpr int kBK2 = 32;
-constexpr int kRow2 = 2 * kBK2;  // bytes per staged row
-// 16-B chunk c of row r sits at chunk c ^ ((r >> 1) & 3): the 16-lane groups
-// of ds_read_b128 (rows 16 x + c, chunk q) hit 16 distinct bank quads
-__device__ __forceinline__ int lds_chunk2(int row, int cl) { return cl ^ ((row >> 1) & 3); }
-__device__ __forceinline__ bf16x8 frag2(const char LDSP *base, int row, int cl) {
-  return *reinterpret_cast<const bf16x8 LDSP *>(base + row * kRow2 + (lds_chunk2(row, cl) << 4));
-}
-template <int TS, int NT, int NW>
-__device__ __forceinline__ void stage_issue2(const H16Args &a, char LDSP *buf, int v0, int m0,
-                                             int k0, int wid, int lane) {
-  constexpr int SA = 16 * TS, BNp = 16 * NT, PW = BNp / 16, PIECES = (BNp + kBM) / 16;
-  const int rl = lane >> 2, p = lane & 3;
-#pragma unroll
-  for (int i0 = 0; i0 < PIECES; i0 += NW) {
-    const int i = i0 + wid;
-    if (i < PIECES) {  // wave-uniform
-      const uint16_t *src;
-      int r;
-      if (i < PW) {
-        r = 16 * i + rl;
-        const int s = r / SA, j = r - s * SA;
-        const int v = v0 + s;
-        const int wr = (v < a.V && j < a.A) ? v * a.A + j : v0 * a.A;  // pad rows: any row
-        src = a.w + (int64_t)wr * a.K;
-      } else {
-        r = 16 * (i - PW) + rl;
-        src = a.h + (int64_t)min(m0 + r, a.B - 1) * a.K;
-      }
-      src += k0 + 8 * lds_chunk2(r, p);
-      char LDSP *dst = buf + (i < PW ? 0 : BNp * kRow2) + (r - rl) * kRow2;
-      __builtin_amdgcn_global_load_lds((const GLBP void *)src, (LDSP void *)dst, 16, 0, 0);
-    }
-  }
-}
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int TS, bool BWD, int NW, int NS>
-__global__ __launch_bounds__(64 * NW, NW / 4) void k_hg16d(H16Args a) {
-  constexpr int S = kMaxNT / TS, NT = S * TS, SA = 16 * TS, BNp = 16 * NT;
-  constexpr int MC = 16 / NW, kThreads = 64 * NW;
-  constexpr int kStageW = BNp * kRow2, kStage = kStageW + kBM * kRow2;
-  constexpr int PIECES = (BNp + kBM) / 16, PF = PIECES / NW, PR = PIECES % NW;
-  extern __shared__ __align__(16) char lds_raw[];
-  char LDSP *lds = (char LDSP *)lds_raw;
-  float LDSP *biasL = reinterpret_cast<float LDSP *>(lds + NS * kStage);
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int q = lane >> 4, c = lane & 15;
-  int n_tile, g;
-  if (!hg16_tile(a, n_tile, g)) return;
-  const int v0 = n_tile * S;
-  const bool dsum = BWD && a.dpart;
-  float LDSP *colL = dsum ? biasL + BNp + wid * BNp : nullptr;
-  for (int n = t; n < BNp; n += kThreads) {
-    const int s = n / SA, j = n - s * SA, v = v0 + s;
-    biasL[n] = (v < a.V && j < a.A) ? a.bias[v * a.A + j] : 0.f;
-  }
-  if (dsum)
-    for (int n = t; n < NW * BNp; n += kThreads) biasL[BNp + n] = 0.f;
-  const int nk = a.K / kBK2;
-  const int nblk = (a.m_blocks - g + a.m_groups - 1) / a.m_groups;
-  const int total = nblk * nk;
-  // stage st: K step st % nk of the workgroup's M block st / nk
-  auto issue = [&](int st) {
-    const int bi = st / nk;
-    stage_issue2<TS, NT, NW>(a, lds + (st % NS) * kStage, v0, (g + bi * a.m_groups) * kBM,
-                             (st - bi * nk) * kBK2, wid, lane);
-  };
-#pragma unroll
-  for (int st = 0; st < NS - 1; st++)
-    if (st < total) issue(st);
-  f32x4 acc[NT][MC];
-  __syncthreads();  // biasL
-#pragma unroll
-  for (int nt = 0; nt < NT; nt++) {
-    const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
-#pragma unroll
-    for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
-  }
-#pragma unroll 1
-  for (int st = 0; st < total; st++) {
-    // stage st landed (this wave's pieces; up to NS - 2 later stages stay in
-    // flight: PF or PF + 1 pieces each), then visible to every wave
-    if (st + NS - 2 < total) {
-      if (wid < PR) wait_vmcnt<(NS - 2) * (PF + 1)>();
-      else wait_vmcnt<(NS - 2) * PF>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    __syncthreads();
-    // the stage consumed in step st - 1 is free for step st + NS - 1
-    if (st + NS - 1 < total) issue(st + NS - 1);
-    const char LDSP *cur = lds + (st % NS) * kStage;
-    const char LDSP *Hs = cur + kStageW;
-    constexpr int kPipe = VMP_HG16_PIPE;
-    bf16x8 hf[MC];
-#pragma unroll
-    for (int mc = 0; mc < MC; mc++) hf[mc] = frag2(Hs, 16 * (MC * wid + mc) + c, q);
-    bf16x8 wf[kPipe];
-#pragma unroll
-    for (int i = 0; i < kPipe; i++) wf[i] = frag2(cur, 16 * i + c, q);
-    __builtin_amdgcn_sched_group_barrier(0x100, MC + kPipe, 0);
-#pragma unroll
-    for (int nt = 0; nt < NT; nt++) {
-#pragma unroll
-      for (int mc = 0; mc < MC; mc++)
-        acc[nt][mc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt % kPipe], hf[mc], acc[nt][mc], 0, 0, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, MC, 0);
-      if (nt + kPipe < NT) {
-        wf[nt % kPipe] = frag2(cur, 16 * (nt + kPipe) + c, q);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-    }
-    const int bi = st / nk;
-    if (st - bi * nk == nk - 1) {  // the M block's last K step: its epilogue
-#ifdef VMP_HG16_GEMM_ONLY
-#pragma unroll
-      for (int nt = 0; nt < NT; nt++)
-#pragma unroll
-        for (int mc = 0; mc < MC; mc++) asm volatile("" ::"v"(acc[nt][mc]));
-#else
-      hg16_epilogue<TS, BWD, NW>(a, acc, (g + bi * a.m_groups) * kBM, v0, wid, lane, colL);
-#endif
-#pragma unroll
-      for (int nt = 0; nt < NT; nt++) {
-        const f32x4 b4 = *reinterpret_cast<const f32x4 LDSP *>(biasL + 16 * nt + 4 * q);
-#pragma unroll
-        for (int mc = 0; mc < MC; mc++) acc[nt][mc] = b4;
-      }
-    }
-  }
-  if (dsum) hg16_dsum_flush<TS, NW>(a, biasL + BNp, v0, g);
-}
-
 // stages, the tile's bias, the 8 waves' bias-gradient column sums (backward)
 template <int TS>
 constexpr size_t lds_bytes() {
   return 2 * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
 }
-template <int TS, int NS>
-constexpr size_t lds_bytes_pp() {
-  return NS * (size_t)(16 * (kMaxNT / TS * TS) + kHB) * kRow + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
-}
-template <int TS, int NS>
-constexpr size_t lds_bytes_deep() {
-  return NS * (size_t)(16 * (kMaxNT / TS * TS) + kBM) * kRow2 + 9 * 16 * (kMaxNT / TS * TS) * sizeof(float);
-}
 static_assert(lds_bytes<1>() <= 160 * 1024, "stages exceed LDS");
-static_assert(lds_bytes_pp<1, 3>() <= 160 * 1024, "ping-pong stages exceed LDS");
-#ifndef VMP_HG16_NS
-#define VMP_HG16_NS 4  // deep kernel's LDS stages
-#endif
-static_assert(lds_bytes_deep<1, VMP_HG16_NS>() <= 160 * 1024, "deep stages exceed LDS");
 
 int pick_ts(int A) { return (A + 15) / 16; }  // segment width: 16 TS columns, TS = ceil(A / 16)
 
@@ -1228,118 +699,24 @@ hipError_t launch_ts(const H16Args &a, int TS, hipStream_t st) {
   const int64_t n_wg = a.team > 0 ? (int64_t)(a.teams + 7) / 8 * 8 * a.team
                                   : (int64_t)a.n_tiles * a.m_groups;
   const dim3 grid((unsigned)n_wg), block(64 * NW);
-  if (SMP) {  // sampling: the two-stage kernel only
-    switch (TS) {
-#define VMP_HG16S_CASE(T) \
-  case T: hipLaunchKernelGGL((k_hg16<T, false, NW, true>), grid, block, lds_bytes<T>(), st, a); break;
-      VMP_HG16S_CASE(1) VMP_HG16S_CASE(2) VMP_HG16S_CASE(3) VMP_HG16S_CASE(4)
-      VMP_HG16S_CASE(5) VMP_HG16S_CASE(6) VMP_HG16S_CASE(7)
-      default: hipLaunchKernelGGL((k_hg16<8, false, NW, true>), grid, block, lds_bytes<8>(), st, a); break;
-#undef VMP_HG16S_CASE
-    }
-    return hipGetLastError();
-  }
-  // VMP_HG16_DEEP=1: the BK = 32 multi-stage kernel (measured slower: forward
-  // 10.3 vs 9.06 ms, backward 14.8 vs 13.3 ms at NS 4 and 5, r04_hg16_deep.log)
-  const char *dp = getenv("VMP_HG16_DEEP");
-  if (dp && dp[0] == '1') {
-    constexpr int NS = VMP_HG16_NS;
-    switch (TS) {
-#define VMP_HG16D_CASE(T) \
-  case T: hipLaunchKernelGGL((k_hg16d<T, BWD, NW, NS>), grid, block, (lds_bytes_deep<T, NS>()), st, a); break;
-      VMP_HG16D_CASE(1) VMP_HG16D_CASE(2) VMP_HG16D_CASE(3) VMP_HG16D_CASE(4)
-      VMP_HG16D_CASE(5) VMP_HG16D_CASE(6) VMP_HG16D_CASE(7)
-      default: hipLaunchKernelGGL((k_hg16d<8, BWD, NW, NS>), grid, block, (lds_bytes_deep<8, NS>()), st, a); break;
-#undef VMP_HG16D_CASE
-    }
-    return hipGetLastError();
-  }
-  // VMP_HG16_PP=2 / 3: the ping-pong kernel with 2 / 3 LDS stages
-  const char *pp = getenv("VMP_HG16_PP");
-  if (pp && (pp[0] == '2' || pp[0] == '3')) {  // its LDS stages
-    const bool s3 = pp[0] == '3';
-    switch (TS) {
-#define VMP_HG16P_CASE(T)                                                                        \
-  case T:                                                                                        \
-    if (s3) hipLaunchKernelGGL((k_hg16p<T, BWD, 3>), grid, dim3(512), (lds_bytes_pp<T, 3>()), st, a); \
-    else hipLaunchKernelGGL((k_hg16p<T, BWD, 2>), grid, dim3(512), (lds_bytes_pp<T, 2>()), st, a);    \
-    break;
-      VMP_HG16P_CASE(1) VMP_HG16P_CASE(2) VMP_HG16P_CASE(3) VMP_HG16P_CASE(4)
-      VMP_HG16P_CASE(5) VMP_HG16P_CASE(6) VMP_HG16P_CASE(7)
-      default: VMP_HG16P_CASE(8)
-#undef VMP_HG16P_CASE
-    }
-    return hipGetLastError();
-  }
   switch (TS) {
 #define VMP_HG16_CASE(T) \
-  case T: hipLaunchKernelGGL((k_hg16<T, BWD, NW>), grid, block, lds_bytes<T>(), st, a); break;
+  case T: hipLaunchKernelGGL((k_hg16<T, BWD, NW, SMP>), grid, block, lds_bytes<T>(), st, a); break;
     VMP_HG16_CASE(1) VMP_HG16_CASE(2) VMP_HG16_CASE(3) VMP_HG16_CASE(4)
     VMP_HG16_CASE(5) VMP_HG16_CASE(6) VMP_HG16_CASE(7)
-    default: hipLaunchKernelGGL((k_hg16<8, BWD, NW>), grid, block, lds_bytes<8>(), st, a); break;
+    default: hipLaunchKernelGGL((k_hg16<8, BWD, NW, SMP>), grid, block, lds_bytes<8>(), st, a); break;
 #undef VMP_HG16_CASE
   }
   return hipGetLastError();
 }
 
-// The resident-W kernel when its slab fits LDS: S = 8 / TS segments per
-// column tile, 512-sample M blocks, G M groups (a multiple of 8, one XCD's
-// workgroups per group at a time) whose n_tiles x G workgroups fill the last
-// one-per-CU dispatch round best.
-template <bool BWD>
-bool launch_res(H16Args &a, int TS, hipStream_t st, hipError_t &err) {
-  const char *rs = getenv("VMP_HG16_RES");
-  if (!(rs && rs[0] == '1')) return false;
-  const int S = 8 / TS;
-  const size_t lds = (size_t)16 * S * TS * 2 * a.K + 9 * 16 * S * TS * sizeof(float);
-  if (lds > 160 * 1024) return false;
-  a.n_tiles = (a.V + S - 1) / S;
-  a.m_blocks = (a.B + kRBM - 1) / kRBM;
-  int best = 8;
-  double best_eff = -1.0;
-  for (int G = 8; G <= 512 && (G <= a.m_blocks || G == 8); G += 8) {
-    const int64_t wg = (int64_t)a.n_tiles * G;
-    const double eff = (double)wg / ((double)((wg + 255) / 256) * 256.0);
-    if (eff > best_eff + 1e-9) {
-      best_eff = eff;
-      best = G;
-    }
-    if (eff > 0.97) break;
-  }
-  a.m_groups = best;
-  a.team = 0;
-  const char *sg = getenv("VMP_HG16_STAG");
-  a.stag = sg ? atoi(sg) : 4;
-  const dim3 grid((unsigned)((int64_t)a.n_tiles * best)), block(512);
-  const char *rde = getenv("VMP_HG16_RD");  // h chunks in flight: 2 (default) or 4 (spills)
-  const bool rd4 = (a.K / 32) % 4 == 0 && rde && rde[0] == '4';
-  switch (TS) {
-#define VMP_HG16R_CASE(T)                                                              \
-  case T:                                                                              \
-    if (rd4) hipLaunchKernelGGL((k_hg16r<T, BWD, 4>), grid, block, lds, st, a);        \
-    else hipLaunchKernelGGL((k_hg16r<T, BWD, 2>), grid, block, lds, st, a);            \
-    break;
-    VMP_HG16R_CASE(1) VMP_HG16R_CASE(2) VMP_HG16R_CASE(3) VMP_HG16R_CASE(4)
-    VMP_HG16R_CASE(5) VMP_HG16R_CASE(6) VMP_HG16R_CASE(7)
-    default: VMP_HG16R_CASE(8)
-#undef VMP_HG16R_CASE
-  }
-  err = hipGetLastError();
-  return true;
-}
-
 template <bool BWD, bool SMP = false>
 hipError_t launch_hg16(H16Args &a, hipStream_t st) {
   const int TS = pick_ts(a.A);
-  if (!SMP) {
-    hipError_t e;
-    if (launch_res<BWD>(a, TS, st, e)) return e;
-  }
   const int S = kMaxNT / TS;
   a.n_tiles = (a.V + S - 1) / S;
   a.m_blocks = (a.B + kBM - 1) / kBM;
-  const char *te = getenv("VMP_HG16_TEAM");
-  const int team = te ? atoi(te) : 8;
+  const int team = kTeam;
   a.team = 0;
   if (team > 0 && a.m_blocks >= team) {
     // r walks per team member: the grid n_tiles x team x r (rounded to whole
@@ -1374,9 +751,13 @@ int check_common(int32_t B, int32_t K, int32_t V, int32_t A, const void *h, cons
     return policy_fail(VMP_EINVAL, "bf16 actor head: needs K % 64 == 0 and A <= 128");
   if ((((uintptr_t)h) | ((uintptr_t)w)) & 15)
     return policy_fail(VMP_EINVAL, "bf16 actor head: h and weight must be 16-byte aligned");
-  // the epilogue reads a row's ceil(A / 32) mask words as one u32x4 / u32x2
-  if (((uintptr_t)bits) & 15)
-    return policy_fail(VMP_EINVAL, "bf16 actor head: mask_bits must be 16-byte aligned");
+  // the epilogue reads a row's W32 = ceil(A / 32) mask words as one u32x4
+  // (W32 = 4) or u32x2 (W32 = 2), else word by word; rows are W32 words apart,
+  // so the base alignment of that vector width is all it needs
+  const int W32 = (A + 31) / 32;
+  const uintptr_t need = W32 == 4 ? 15 : (W32 == 2 ? 7 : 3);
+  if (((uintptr_t)bits) & need)
+    return policy_fail(VMP_EINVAL, "bf16 actor head: mask_bits misaligned for its row width");
   return VMP_OK;
 }
 

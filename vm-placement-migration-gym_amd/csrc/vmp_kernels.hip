@@ -1026,12 +1026,8 @@ __device__ __forceinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, 
   for (int i = lane; i < P; i += 64) L.ord[i] = (uint16_t)i;
   const int hi = P - above - 1, lo = P - above - eq;
   wsync();
-#ifdef VMP_SERIAL_SORT
-  if (lane == 0) aquicksort_lds(KeySum{L.fcpu, L.fmem}, L.ord, P, L.sortstk, lo, hi);
-#else
   wave_aquicksort(KeySum{L.fcpu, L.fmem}, L.ord, P, L.sortstk, lo, hi,
                   reinterpret_cast<uint16_t LDSP *>(L.sortstk + 256));
-#endif
   wsync();
   for (int b = hi; b >= lo; b -= 64) {  // visiting order: descending positions
     const int pos = b - lane;
@@ -1220,12 +1216,8 @@ __device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, const 
   // previous per-step launch) only gates this speculation: a draw it wrongly
   // skipped would come from svc_fallback, from the same stream position.
   const uint64_t hint = H->pad;
-#ifndef VMP_NO_DRAW_HINT
   const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 0x1FFFFFFFu) == 0 &&
                          (uint32_t)hint > (uint32_t)H->timestep + 1u;
-#else  // A/B switch
-  const bool none_free = false && hint;
-#endif
   const int S = none_free ? 0 : (int)(need < p.scap ? need : p.scap);
   g.base = r4.s;
   g.inc = r4.inc;
@@ -1963,7 +1955,10 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   bool skip_time = false;
   uint32_t nf_carry = 0u;
   if (ONE && !EXT) {
-#ifndef VMP_NO_TIME_SKIP
+    // (off in the check build: its quiet steps still run the fit loop and
+    // may place, which a skipped step's carried nf and zero finish bits
+    // would leave stale: the audited state must evolve as the product's)
+#if !defined(VMP_NO_TIME_SKIP) && !defined(VMP_CHECK_QUIET)
     const uint64_t ph = L.hdr->pad;
     nf_carry = (uint32_t)ph;
     skip_time = ((ph >> 62) & 1u) && (ph >> 63) && ((ph >> 32) & 0x1FFFFFFFu) == 0u &&
@@ -2129,7 +2124,6 @@ __global__ __launch_bounds__(64 * kEnvWavesPerBlock, VMP_WAVES_PER_EU_ONE) void 
   env_body<VPT, true, true>(p, o);
 }
 
-#ifndef VMP_BIG_ONLY  // (-DVMP_BIG_ONLY: register experiments on k_env_big alone)
 template __global__ void k_env_ext<1>(EnvParams, StepOut);
 template __global__ void k_env_ext<2>(EnvParams, StepOut);
 template __global__ void k_env_ext<4>(EnvParams, StepOut);
@@ -2145,7 +2139,6 @@ template __global__ void k_env<8, false>(EnvParams, StepOut);
 template __global__ void k_env<8, true>(EnvParams, StepOut);
 template __global__ void k_env<16, false>(EnvParams, StepOut);
 template __global__ void k_env<16, true>(EnvParams, StepOut);
-#endif
 
 // ------------------------------------------------------------- reset -----
 // VmEnv.reset (env.py:180-226) for masked envs, one wave per env.
@@ -2318,17 +2311,11 @@ __global__ void k_mask_bool(int64_t rows, int A, int W, const uint32_t *bits, ui
 // applied by wave 0 in that order. Same arithmetic, same
 // order as k_env: the two kernels are interchangeable (VMP_BIG_KERNEL=1
 // forces this one for any V, which the parity tests use).
-// Slot-row loops of the block kernel (s = 0..SPT-1), unrolled by 4 (a full
-// unroll, -DVMP_BIG_UNROLL, hoists enough per-slot temporaries to grow the
-// scratch from 496 to 3296 B per lane at SPT = 20; -DVMP_BIG_ROLLED keeps one
-// row per iteration, one LDS round trip per row).
-#ifdef VMP_BIG_UNROLL
-#define VMP_SLOOP _Pragma("unroll")
-#elif defined(VMP_BIG_ROLLED)
-#define VMP_SLOOP _Pragma("unroll 1")
-#else  // 4 slot rows per iteration: 4 LDS reads in flight per round trip
+// Slot-row loops of the block kernel (s = 0..SPT-1), unrolled by 4: 4 LDS
+// reads in flight per round trip (a full unroll hoists enough per-slot
+// temporaries to grow the scratch from 496 to 3296 B per lane at SPT = 20;
+// one row per iteration costs one LDS round trip per row).
 #define VMP_SLOOP _Pragma("unroll 4")
-#endif
 
 // k_env_big's workgroup: 6 waves (two workgroups per CU at 3 waves/SIMD); a
 // compile-time thread count so slot s of a thread sits at a constant LDS
@@ -2346,11 +2333,8 @@ static_assert(kBigNT % 64 == 0 && kBigNT <= 512 && kBigMaxSPT <= 64, "block shap
 // k_env_big's per-step helpers (pairwise-sum jobs, reward, draws): inlined
 // (round 3: out of line, every call saved and restored the caller's live
 // registers through scratch, 224 B per lane; inlined the kernel needs 193
-// VGPRs instead of 250 and runs 8 % faster with the 4-row slot loops);
-// -DVMP_BIG_CALL=__noinline__ restores the calls (A/B build)
-#ifndef VMP_BIG_CALL
+// VGPRs instead of 250 and runs 8 % faster with the 4-row slot loops)
 #define VMP_BIG_CALL __forceinline__
-#endif
 struct BigShared {
   int32_t wcnt[16];   // per-wave counts of a compaction
   int32_t bc[8];      // broadcast scalars
@@ -3179,19 +3163,14 @@ __device__ __forceinline__ double big_tail(const EnvParams &p, const Lds &L, con
   SMask fterm = 0;
   // this thread's VM words, in registers for the tail's per-slot passes (the
   // LDS copy W stays current for the cross-thread readers: frees, obs, mask)
-#ifdef VMP_BIG_REG_WR
-  uint32_t wr[SPT];
-#pragma unroll
-  for (int s = 0; s < SPT; s++) wr[s] = W[s * NT + t];
-#else  // the tail reads its words from LDS: a 40-register copy (-DVMP_BIG_REG_WR)
-       // pushed the kernel to 256 VGPRs and spilled SGPRs to scratch
-       // (~49 KB of scratch traffic each way per env-step), 2 % slower
+  // (the tail reads its words from LDS: a 40-register copy pushed the kernel
+  // to 256 VGPRs and spilled SGPRs to scratch, ~49 KB of scratch traffic
+  // each way per env-step, 2 % slower)
   struct {
     uint32_t LDSP *W;
     int t;
     __device__ __forceinline__ uint32_t LDSP &operator[](int s) const { return W[s * kBigNT + t]; }
   } wr{W, t};
-#endif
   {
     uint32_t hw[SPT];  // the time words, issued together, dead after this loop
 #pragma unroll
@@ -3262,9 +3241,6 @@ VMP_SLOOP
   for (int s = 0; s < SPT; s++)
     if ((fterm >> s) & 1u) {
       wr[s] = w_make(NUL, 0, 0);
-#ifdef VMP_BIG_REG_WR
-      W[s * NT + t] = wr[s];
-#endif
     }
   STAMP(2);
   if (w0 && !clamp_inline)
@@ -3317,9 +3293,6 @@ VMP_SLOOP
         if (((fnull >> s) & 1u) && j >= j0 && j < j1) {
           const int cc = acc_g ? gsc[j] : L.accc[j], cm = acc_g ? gsc[p.V + j] : L.accm[j];
           wr[s] = w_make(WAIT, cc, cm);
-#ifdef VMP_BIG_REG_WR
-          W[s * NT + t] = wr[s];
-#endif
           ST_NT(vw32 + vm_time_idx(s * NT + t), (uint32_t)L.evt[j - j0]);
           dirty |= SBIT(s);
         }
@@ -3384,7 +3357,6 @@ VMP_SLOOP
 #ifdef VMP_WGTIME
     STAMP(17);  // wave 0: obs issued
 #endif
-#if !defined(VMP_ABL_NOA) && !defined(VMP_ABL_NOB) && !defined(VMP_KL_PHASES)
     // kl on four waves: chained, no phase barrier. Only wave 0 owns the LDS
     // plan of the deep pairwise sums, so the chains need every job of waves
     // 1-3 within the register plan (n <= pw_reg_cap): at P1000 / V10000
@@ -3395,19 +3367,11 @@ VMP_SLOOP
       big_kl_sums(p, T, L.base, B, (int)k, n_ex, spill, kstep + 1);
       STAMP(20);
       STAMP(21);
-    } else
-#endif
-    {
-#ifndef VMP_ABL_NOA  // timing ablations only (rewards wrong): -DVMP_ABL_NOA / -DVMP_ABL_NOB
-    if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, kBigSplitA, true, spill);
-#else
-    __syncthreads();
-#endif
-    STAMP(20);
-#ifndef VMP_ABL_NOB
-    if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true, false, spill);
-#endif
-    STAMP(21);
+    } else {
+      if (ja) big_sum_phase(p, T, L.base, B, ja, (int)k, n_ex, kBigSplitA, true, spill);
+      STAMP(20);
+      if (kl) big_sum_phase(p, T, L.base, B, 0x3C0u, (int)k, n_ex, true, false, spill);
+      STAMP(21);
     }
   }
   if (w0) big_stats_final(p, B, L.base, k, n_ex, n_w, n_term, arrivals);
@@ -3589,12 +3553,10 @@ template <bool ONE>
 static void launch_big_one(int spt, int n_env, size_t lds, hipStream_t s, const EnvParams &p,
                            const StepOut &o) {
   const dim3 grid(n_env), block(kBigNT);
-#ifndef VMP_BIG_ONLY
   if (spt == 4) hipLaunchKernelGGL((k_env_big<4, ONE>), grid, block, lds, s, p, o);
   else if (spt == 8) hipLaunchKernelGGL((k_env_big<8, ONE>), grid, block, lds, s, p, o);
   else if (spt == 16) hipLaunchKernelGGL((k_env_big<16, ONE>), grid, block, lds, s, p, o);
   else
-#endif
   hipLaunchKernelGGL((k_env_big<kBigMaxSPT, ONE>), grid, block, lds, s, p, o);
 }
 // host side: the block kernel's geometry and launcher (vmp_capi.cpp)
@@ -3611,11 +3573,9 @@ void launch_big_env(int spt, bool one, int n_env, size_t lds, hipStream_t s, con
 // its static LDS
 int big_occupancy(int spt, size_t lds, int *static_lds) {
   const void *f = reinterpret_cast<const void *>(&k_env_big<kBigMaxSPT, true>);
-#ifndef VMP_BIG_ONLY
   if (spt == 4) f = reinterpret_cast<const void *>(&k_env_big<4, true>);
   else if (spt == 8) f = reinterpret_cast<const void *>(&k_env_big<8, true>);
   else if (spt == 16) f = reinterpret_cast<const void *>(&k_env_big<16, true>);
-#endif
   hipFuncAttributes a;
   if (hipFuncGetAttributes(&a, f) == hipSuccess) *static_lds = (int)a.sharedSizeBytes;
   int nb = -1;

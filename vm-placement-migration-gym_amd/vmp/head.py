@@ -241,11 +241,19 @@ def actor_head_bf16_supported(K, A):
     return K % 64 == 0 and A <= ACTOR_HEAD_MAX_A
 
 
+def bf16_bits_align_mask(A):
+    """Address bits that must be 0 in the mask-bits base pointer of the bf16 head
+    kernels: a row of W32 = ceil(A/32) words is read as one u32x4 (W32 = 4,
+    16 B) or u32x2 (W32 = 2, 8 B), else word by word (4 B)."""
+    w32 = (A + 31) // 32
+    return 15 if w32 == 4 else (7 if w32 == 2 else 3)
+
+
 def _bf16_operands(hb, wb, bias, V, A, bits, action, who):
     """Shape / dtype / layout contract of vmp_actor_head_bf16_fwd/_bwd
     (include/vmp.h): contiguous bf16 h [B, K] and weight [V*A, K], 16-byte
     aligned; f32 bias [V*A]; mask bits contiguous int32 [B, V, ceil(A/32)]
-    with 16-byte aligned rows of the vector loads; actions as contiguous
+    aligned to the row's vector load (bf16_bits_align_mask); actions as contiguous
     int32 [B, V] (cast here, as the forward always did)."""
     _need_device(hb, who)
     if hb.dim() != 2 or hb.dtype != torch.bfloat16 or not hb.is_contiguous():
@@ -261,8 +269,9 @@ def _bf16_operands(hb, wb, bias, V, A, bits, action, who):
         if (tuple(bits.shape) != (B, V, (A + 31) // 32) or bits.dtype != torch.int32
                 or not bits.is_contiguous()):
             raise ValueError(f"{who}: mask bits must be contiguous int32 {(B, V, (A + 31) // 32)}")
-        if bits.data_ptr() & 15:
-            raise ValueError(f"{who}: mask bits must be 16-byte aligned")
+        if bits.data_ptr() & bf16_bits_align_mask(A):
+            raise ValueError(f"{who}: mask bits misaligned for the row's "
+                             f"{(A + 31) // 32}-word vector load")
     act = action.to(device=hb.device, dtype=torch.int32).reshape(B, V).contiguous()
     return B, K, act
 

@@ -67,11 +67,12 @@ class PPOConfig:
     value_loss_broadcast: bool = True  # ppo.py:266-270 [mb,1]-[mb] broadcast
     precision: str = "f32"             # "bf16": bf16 GEMM inputs, f32 accumulate/output
     chunk_bytes: int = 0               # logits budget per update chunk (0: from free HBM, fixed at the first update)
-    # bf16 fused head: dlogits bytes per backward chunk. 16 GiB holds a whole
-    # 204 800-row minibatch at V*A = 30 600 (12.5 GB): one dW / dh GEMM pair
-    # per minibatch instead of three, update 0.743 -> 0.718 s
-    # (profiles/r05_dlogits_chunk_ab.log); the peak grows by the same 8 GB
-    dlogits_chunk_bytes: int = 1 << 34
+    # bf16 fused head: dlogits bytes per backward chunk (0: from free HBM,
+    # fixed at the first update: min(16 GiB, free / 2 / ranks sharing the
+    # device)). 16 GiB holds a whole 204 800-row minibatch at V*A = 30 600
+    # (12.5 GB): one dW / dh GEMM pair per minibatch instead of three, update
+    # 0.743 -> 0.718 s (profiles/r05_dlogits_chunk_ab.log)
+    dlogits_chunk_bytes: int = 0
     kl_lookahead: bool = True          # step before the KL early-stop flag reaches the host,
                                        # roll back on a break (same accepted steps)
     seed_stride: int = 4               # env/episode reset seed spacing
@@ -256,19 +257,27 @@ def _host_scalar(t):
     return read
 
 
-BF16_MIN_OUT = 16  # narrower Linears (the critic's value head) stay f32
+DLOGITS_CHUNK_MAX = 1 << 34  # the dlogits budget's cap (16 GiB)
+
+
+def _keep_f32(layer):
+    """Mark a Linear that stays f32 in the bf16 leg (the critic's value head)."""
+    layer._vmp_keep_f32 = True
+    return layer
 
 
 def _run_mlp(seq, x, precision):
-    """seq(x); in bf16 precision every Linear of >= BF16_MIN_OUT outputs runs as
-    BF16Linear. The critic's 512 -> 1 value head stays an f32 Linear: its
+    """seq(x); in bf16 precision every Linear runs as BF16Linear except the one
+    marked by _keep_f32, the critic's 512 -> 1 value head, which stays an f32
+    Linear (a width threshold would also move every layer of a small-hidden
+    model to f32). Its
     GEMV is a bandwidth-bound 2 KB-per-row read, and hipBLASLt's bf16 -> f32
     addmm at N = 1 costs ~17 ms of host time per call on ROCm 7 / torch 2.10
     (tools/host_prof_values.py), which serialised the update's value pass."""
     if precision != "bf16":
         return seq(x)
     for m in seq:
-        if isinstance(m, nn.Linear) and m.out_features >= BF16_MIN_OUT:
+        if isinstance(m, nn.Linear) and not getattr(m, "_vmp_keep_f32", False):
             x = BF16Linear.apply(x, m.weight, m.bias)
         else:
             x = m(x)
@@ -295,7 +304,7 @@ class Network(nn.Module):
         self.critic = nn.Sequential(
             ortho_init(nn.Linear(input_size, hidden_size, dtype=dtype)), nn.Tanh(),
             ortho_init(nn.Linear(hidden_size, hidden_size, dtype=dtype)), nn.Tanh(),
-            ortho_init(nn.Linear(hidden_size, 1, dtype=dtype), scale=1))
+            _keep_f32(ortho_init(nn.Linear(hidden_size, 1, dtype=dtype), scale=1)))
         self.actor = nn.Sequential(
             ortho_init(nn.Linear(input_size, hidden_size, dtype=dtype)), nn.Tanh(),
             ortho_init(nn.Linear(hidden_size, hidden_size, dtype=dtype)), nn.Tanh(),
@@ -355,7 +364,8 @@ class Network(nn.Module):
         applies (VMP_BF16_SAMPLE=0: the logits path, for A/B measurement)."""
         return (obs.is_cuda and self.bf16_fused()
                 and os.environ.get("VMP_BF16_SAMPLE", "1") != "0"
-                and (bits is None or (bits.is_contiguous() and bits.data_ptr() % 16 == 0)))
+                and (bits is None or (bits.is_contiguous()
+                                      and (bits.data_ptr() & H.bf16_bits_align_mask(self.A)) == 0)))
 
     def det(self, obs):
         """get_det_action's argmax (ppo.py:128-131) -> int32 [B, V]."""
@@ -386,7 +396,7 @@ class Network(nn.Module):
         head = 8 * self.V if self.bf16_fused() else 4 * self.V * self.A
         return head + 40 * H
 
-    def logprob_entropy(self, obs, bits, action, dlogits_chunk_bytes=1 << 34):
+    def logprob_entropy(self, obs, bits, action, dlogits_chunk_bytes=DLOGITS_CHUNK_MAX):
         """get_action(obs, action, mask)'s logprob and entropy (ppo.py:115-126) for
         the update, differentiable. The bf16 leg with the HIP head runs the last
         Linear and the head as one node: fused on the bf16 matrix cores
@@ -833,7 +843,7 @@ class PPOTrainer:
             o = obs[t0:t1, n0:n1].reshape(mt * nc, -1)
             b = None if bits is None else bits[t0:t1, n0:n1].reshape(mt * nc, self.V, -1)
             a = act[t0:t1, n0:n1].reshape(mt * nc, self.V)
-            newlp, ent = m.logprob_entropy(o, b, a, cfg.dlogits_chunk_bytes)
+            newlp, ent = m.logprob_entropy(o, b, a, self._dlogits_budget(dev))
             newlp = newlp.reshape(mt, nc)
             logratio = newlp - old_lp[t0:t1, n0:n1]
             ratio = torch.exp(logratio)
@@ -897,19 +907,62 @@ class PPOTrainer:
                     for k, v in s.items():
                         opt.state[p][k].copy_(v)
 
+    def _min_over_ranks(self, b, dev):
+        if self.dist:
+            t = torch.tensor([b], dtype=torch.int64, device=dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+            b = int(t.item())
+        return b
+
     def _chunk_budget(self, dev):
         """The update's chunk budget, fixed once per trainer (the chunk count sets
         the f32 gradient summation order, so it must not move with the free
         memory between minibatches or runs); data parallel: the minimum over
         ranks, so every rank chunks alike."""
         if getattr(self, "_budget", None) is None:
-            b = self._chunk_bytes(dev)
-            if self.dist:
-                t = torch.tensor([b], dtype=torch.int64, device=dev)
-                self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
-                b = int(t.item())
-            self._budget = b
+            self._dlogits_budget(dev)  # sized first: the activations get what it leaves
+            self._budget = self._min_over_ranks(self._chunk_bytes(dev), dev)
         return self._budget
+
+    def _device_sharers(self, dev):
+        """Ranks of the group on this process's device (gloo rehearsals put
+        several on one GPU): one all-reduce of each rank's device key."""
+        if not self.dist or dev.type != "cuda":
+            return 1
+        if getattr(self, "_sharers", None) is None:
+            import socket
+            import zlib
+            props = torch.cuda.get_device_properties(dev)
+            ident = getattr(props, "uuid", None)
+            ident = str(ident) if ident is not None else "%s:%s" % (
+                getattr(props, "pci_bus_id", ""), dev.index)
+            key = zlib.crc32(("%s/%s" % (socket.gethostname(), ident)).encode()) + 1
+            keys = torch.zeros(self.world, dtype=torch.int64, device=dev)
+            keys[self.rank] = key
+            self.dist.all_reduce(keys, group=self.group)
+            self._sharers = max(1, int((keys == key).sum().item()))
+        return self._sharers
+
+    def _dlogits_budget(self, dev):
+        """Bytes of bf16 dlogits per fused-head backward chunk: PPOConfig.
+        dlogits_chunk_bytes, or min(16 GiB, half the memory free on the device
+        / the ranks sharing it), fixed at the first update and min-reduced over
+        ranks (the chunking sets dW's summation order)."""
+        if getattr(self, "_dl_budget", None) is None:
+            if int(self.cfg.dlogits_chunk_bytes) > 0:
+                b = int(self.cfg.dlogits_chunk_bytes)
+            elif dev.type != "cuda":
+                b = DLOGITS_CHUNK_MAX
+            else:
+                b = min(DLOGITS_CHUNK_MAX, self._free_bytes(dev) // 2 // self._device_sharers(dev))
+            self._dl_budget = self._min_over_ranks(max(1 << 26, b), dev)
+        return self._dl_budget
+
+    @staticmethod
+    def _free_bytes(dev):
+        """Memory free on the device, incl. blocks torch has cached but not handed out."""
+        free, _ = torch.cuda.mem_get_info(dev)
+        return int(free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))
 
     def _chunk_bytes(self, dev):
         """Logits budget per update chunk: PPOConfig.chunk_bytes, or what the
@@ -920,14 +973,19 @@ class PPOTrainer:
         288 GB MI355X that is 36 GB: a whole config/100.yml minibatch of 8192
         envs (25 GB of f32 logits) is one chunk, so backward writes each
         gradient once instead of accumulating chunk by chunk; on a smaller or
-        shared GPU the chunks shrink instead of running out of memory."""
+        shared GPU the chunks shrink instead of running out of memory (ranks
+        sharing the device split it; the bf16 fused head's dlogits budget is
+        taken off first)."""
         if int(self.cfg.chunk_bytes) > 0:
             return int(self.cfg.chunk_bytes)
         if dev.type != "cuda":
             return 4 << 30
-        free, total = torch.cuda.mem_get_info(dev)
-        free += torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-        return max(1 << 28, min(int(total) // 8, int(free) // 3))
+        _, total = torch.cuda.mem_get_info(dev)
+        free = self._free_bytes(dev)
+        if self.model.bf16_fused():  # the fused head's dlogits chunk comes out of it
+            free -= self._dlogits_budget(dev)
+        n = self._device_sharers(dev)
+        return max(1 << 28, min(int(total) // 8 // n, free // 3 // n))
 
     def _zero_grads(self, params):
         """Single process: grads re-created by backward. Data parallel: every
