@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define VMP_ABI_VERSION 10
+#define VMP_ABI_VERSION 11
 
 #define VMP_OK 0
 #define VMP_EINVAL (-1)
@@ -273,6 +273,40 @@ int vmp_actor_head(int32_t B, int32_t K, int32_t V, int32_t A, int32_t mode, con
                    float wait_ratio, int32_t wait_index, uint64_t seed, uint64_t offset,
                    const uint64_t *rng_counter, int32_t *action, float *logprob, float *entropy,
                    float *logits_out, float *workspace, void *hip_stream);
+
+/* The actor MLP forward (ppo.py:98-109: Linear(D, H), Tanh, Linear(H, H),
+ * Tanh, Linear(H, N)) in f32 for rollouts and eval, one launch: x f32[B][D]
+ * (the observations), b1, b2 f32[H] and b3 f32[N] the biases, `packed` the
+ * three weight matrices (nn.Linear's w1 f32[H][D], w2 f32[H][H], w3 f32[N][H])
+ * in the kernel's MFMA-fragment order, written by vmp_actor_mlp_pack into
+ * vmp_actor_mlp_packed_floats(D, H, N, layers) floats (16-byte aligned); the
+ * caller re-packs whenever a weight changes. layers = 3: out = the logits
+ * f32[B][N]; layers = 2: out = self.actor[:-1](x), the last hidden layer
+ * after its Tanh, f32[B][H] (the big heads of config/100.yml go on to
+ * vmp_actor_head; w3 / b3 unused). 16 rows per workgroup on the f32 matrix
+ * cores, activations kept in LDS between layers. Needs H % 32 == 0, H <= 512,
+ * N <= 512, D <= VMP_ACTOR_MLP_MAX_D. Forward only (no autograd). (ABI 11) */
+#define VMP_ACTOR_MLP_MAX_D 1536
+int64_t vmp_actor_mlp_packed_floats(int32_t D, int32_t H, int32_t N, int32_t layers);
+int vmp_actor_mlp_pack(int32_t D, int32_t H, int32_t N, int32_t layers, const float *w1,
+                       const float *w2, const float *w3, float *packed, void *hip_stream);
+int vmp_actor_mlp_f32(int32_t B, int32_t D, int32_t H, int32_t N, int32_t layers, const float *x,
+                      const float *packed, const float *b1, const float *b2, const float *b3,
+                      float *out, void *hip_stream);
+/* The same MLP with the masked head of vmp_policy_head on its logits in one
+ * launch (ppo.py:98-131 Network.get_action / get_det_action with the
+ * PPOAgent.act WAIT coin, ppo.py:151-156): N = V * A <= 512, A <= 128; modes,
+ * mask bits, coin, rng stream and outputs exactly as vmp_policy_head (the
+ * per-row code is shared, so equal logits draw equal actions and give equal
+ * logprob / entropy, bit for bit); logits_out (nullable, f32[B][V*A]) keeps a
+ * copy of the logits. The logits otherwise never leave the workgroup: one
+ * launch per batched step of the eval loop (base.py:71-86). (ABI 11) */
+int vmp_actor_mlp_head_f32(int32_t B, int32_t D, int32_t H, int32_t V, int32_t A, int32_t mode,
+                           const float *x, const float *packed, const float *b1, const float *b2,
+                           const float *b3, const uint32_t *mask_bits, float wait_ratio,
+                           int32_t wait_index, uint64_t seed, uint64_t offset,
+                           const uint64_t *rng_counter, int32_t *action, float *logprob,
+                           float *entropy, float *logits_out, void *hip_stream);
 
 /* Training side of the fused actor head in bf16: the update's
  * get_action(obs, action, mask) (ppo.py:115-126, called at ppo.py:258) and its

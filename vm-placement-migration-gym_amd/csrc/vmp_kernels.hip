@@ -1216,7 +1216,7 @@ __device__ __forceinline__ void predraw(const EnvParams &p, const Lds &L, const 
   // previous per-step launch) only gates this speculation: a draw it wrongly
   // skipped would come from svc_fallback, from the same stream position.
   const uint64_t hint = H->pad;
-  const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 0x1FFFFFFFu) == 0 &&
+  const bool none_free = K == 1 && (hint >> 63) && ((hint >> 32) & 1u) == 0 &&
                          (uint32_t)hint > (uint32_t)H->timestep + 1u;
   const int S = none_free ? 0 : (int)(need < p.scap ? need : p.scap);
   g.base = r4.s;
@@ -1296,7 +1296,7 @@ template <int VPT>
 __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds &L,
                                                    const Tables &T, uint32_t (&wa)[VPT],
                                                    int policy, int32_t *act_out,
-                                                   uint8_t *valid_out, bool quiet,
+                                                   uint8_t *valid_out, bool quiet, int qkind,
                                                    bool &fit_any STAMP_PARAMS) {
   const int lane = lane_id();
   const int P = p.P, WAIT = p.P;
@@ -1308,13 +1308,19 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
   uint32_t won = 0, bad = 0;
   int64_t n_place = 0;
   fit_any = false;
-  // quiet (EnvHdr::pad bit 62): the previous step found no pending VM that
-  // fits any PM, and since then no VM finished (no PM load fell) and none
-  // arrived (no new pending VM): nothing fits now either, so the heuristic
-  // places nothing and the any-fit table need not be built. The check build
-  // (-DVMP_CHECK_QUIET) builds it anyway and counts the quiet steps in which
-  // some pending VM fits (vmp_debug_quiet_violations): 0 unless a writer of
-  // the env state left a stale bit 62 (see EnvHdr::pad).
+  // quiet: skip the heuristic. qkind 1 (EnvHdr::pad bit 62): the previous
+  // step found no pending VM that fits any PM, and since then no VM finished
+  // (no PM load fell) and none arrived (no new pending VM): nothing fits now
+  // either, so the heuristic places nothing and the any-fit table need not
+  // be built. qkind 2 (bit 60): the previous step's placements were all
+  // invalid in f64 (the f32 observation said they fit: a PM loaded to within
+  // rounding of 1) and nothing finished or arrived, so the step sees the same
+  // observation, makes the same decisions and the env rejects them again -
+  // env_body takes this skip only where no actions / validity flags are
+  // returned. The check build (-DVMP_CHECK_QUIET) runs the heuristic anyway
+  // and counts the skippable steps in which some pending VM fits (qkind 1)
+  // or some placement is valid (qkind 2) (vmp_debug_quiet_violations): 0
+  // unless a writer of the env state left a stale bit (see EnvHdr::pad).
 #ifdef VMP_CHECK_QUIET
   if (ballot(pend != 0)) {
 #else
@@ -1340,7 +1346,7 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
     const bool anyfit = ballot(hit != 0) != 0;
     fit_any = anyfit;
 #ifdef VMP_CHECK_QUIET
-    if (quiet && anyfit && lane == 0)
+    if (quiet && qkind == 1 && anyfit && lane == 0)
       __hip_atomic_fetch_add(gptr(&g_quiet_violations), 1ull, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
 #endif
@@ -1425,6 +1431,11 @@ __device__ __forceinline__ int64_t heuristic_apply(const EnvParams &p, const Lds
       STAMP(19);
     }
   }
+#ifdef VMP_CHECK_QUIET
+  if (quiet && qkind == 2 && n_place > 0 && lane == 0)
+    __hip_atomic_fetch_add(gptr(&g_quiet_violations), 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+#endif
   if (act_out || valid_out) {
     const int ln = fresh_lane();
 #pragma unroll
@@ -1945,7 +1956,8 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   uint32_t hiv[VPT];   // ONE: the finish keys / remaining runtimes, in flight
   uint32_t nf = 0u;  // ONE: smallest finish key running on (EnvHdr::pad hint; 0: unknown)
   bool want_nf = false;
-  // ONE, heuristic: a quiet step (EnvHdr::pad bit 62: it places nothing) whose
+  // ONE, heuristic: a quiet step (EnvHdr::pad bit 62, or bit 60 where no
+  // actions / validity flags are returned: it places nothing) whose
   // hint records the smallest finish key nf of the running VMs (the previous
   // launch left no NULL slot) with nf > t + 1 needs no time word: no VM
   // finishes and none is placed, so every finish bit is 0 and nf carries over
@@ -1961,8 +1973,9 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
 #if !defined(VMP_NO_TIME_SKIP) && !defined(VMP_CHECK_QUIET)
     const uint64_t ph = L.hdr->pad;
     nf_carry = (uint32_t)ph;
-    skip_time = ((ph >> 62) & 1u) && (ph >> 63) && ((ph >> 32) & 0x1FFFFFFFu) == 0u &&
-                nf_carry != 0u && (int32_t)(nf_carry - (uint32_t)L.hdr->timestep) > 1;
+    const bool skip_h = ((ph >> 62) & 1u) || (((ph >> 60) & 1u) && !o.act_out && !o.valid);
+    skip_time = skip_h && (ph >> 63) && ((ph >> 32) & 1u) == 0u && nf_carry != 0u &&
+                (int32_t)(nf_carry - (uint32_t)L.hdr->timestep) > 1;
 #endif
     // issued before the action phase, consumed after it (latency hidden by it)
     const uint32_t GLBP *hb = vlo + 64 + (skip_time ? 0 : lane);
@@ -1973,9 +1986,9 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
   }
   uint32_t *vmo = p.vmw + (int64_t)e * vm_pitch(V);
   const int k_steps = ONE ? 1 : o.k_steps;
-  // EnvHdr::pad bit 62 (see heuristic_apply); the external-action kernel
-  // neither uses nor keeps it
-  bool quiet = !EXT && ((L.hdr->pad >> 62) & 1u);
+  // EnvHdr::pad bits 62 / 60 (qkind 1 / 2, see heuristic_apply); the
+  // external-action kernel neither uses nor keeps them
+  int qkind = EXT ? 0 : (((L.hdr->pad >> 62) & 1u) ? 1 : (((L.hdr->pad >> 60) & 1u) ? 2 : 0));
   bool has_ex = (L.hdr->pad >> 61) & 1u;  // bit 61: some VM exists (read with bit 62 only)
 #pragma unroll 1
   for (int k = 0; k < k_steps; k++) {
@@ -1987,8 +2000,11 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
 #pragma unroll
     for (int s = 0; s < VPT; s++) run0 |= (uint32_t)(w_pl(wa[s]) < P) << s;
     bool fit_any = false;
+    // qkind 2 repeats rejected placements: skipped only where no actions or
+    // validity flags leave this step
+    const bool quiet = qkind == 1 || (qkind == 2 && !act_row && !valid_row);
     if (!EXT)
-      n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row, quiet,
+      n_place = heuristic_apply<VPT>(p, L, T, wa, o.policy, act_row, valid_row, quiet, qkind,
                                      fit_any STAMP_ARGS);
     else {
       // the external kernel loads the time words after its action phase: live
@@ -2036,7 +2052,9 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
     bool calm = false;
     const double r = env_tail<VPT, ONE>(p, L, T, wa, rem, run0, fb, dirty, vmo, k, EXT, quiet,
                                         term, calm, has_ex STAMP_ARGS);
-    quiet = !EXT && !fit_any && calm;
+    // the next step's skip: nothing fit (1), or every placement was rejected
+    // (2); a skipped step passes its kind on while nothing changes
+    qkind = (EXT || !calm) ? 0 : quiet ? qkind : (!fit_any ? 1 : (n_place == 0 ? 2 : 0));
     if (o.reward && lane == 0) gptr(o.reward)[(int64_t)k * p.N + e] = r;
     ndone += term;
   }
@@ -2047,8 +2065,8 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
 #pragma unroll
     for (int s = 0; s < VPT; s++) wt[s] = wa[s];
     bool fit_any;
-    heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr, quiet,
-                         fit_any STAMP_ARGS);
+    heuristic_apply<VPT>(p, L, T, wt, o.policy, o.act_out + (int64_t)e * V, nullptr, qkind == 1,
+                         qkind, fit_any STAMP_ARGS);
   }
   STAMP(0);
   if (o.obs) write_obs<VPT>(p, L, T, wa, o.obs + (int64_t)e * p.D);
@@ -2097,7 +2115,8 @@ __device__ __forceinline__ void env_body(const EnvParams &p, const StepOut &o) {
         }
         hint = (1ull << 63) | ((uint64_t)nn << 32) | m;
       }
-      hint |= ((uint64_t)quiet << 62) | ((uint64_t)has_ex << 61);
+      hint |= ((uint64_t)(qkind == 1) << 62) | ((uint64_t)(qkind == 2) << 60) |
+              ((uint64_t)has_ex << 61);
       wsync();
       if (lane == 0) L.hdr->pad = hint;
       wsync();
@@ -2593,7 +2612,6 @@ __device__ __forceinline__ int big_choose(const EnvParams &p, const Lds &L, bool
   int above = 0, eq = 0;
   {
     const int q0 = 16 * lane;
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       const float key = kfc[j >> 2][j & 3] + kfm[j >> 2][j & 3];

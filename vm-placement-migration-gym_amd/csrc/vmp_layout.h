@@ -66,12 +66,16 @@ struct alignas(16) EnvHdr {
   int64_t total_requests, served, suspend_action, place_action, dropped;
   double total_cpu_req, total_mem_req, waiting_ratio, tcm, tmm;
   // per-step kernels' hint for the next launch's draws (predraw): bit 63
-  // valid, bits 32..60 NULL slots after the step, bits 0..31 the smallest
+  // valid, bit 32 some NULL slot after the step, bits 0..31 the smallest
   // finish key of the VMs still running (0: no hint). Bit 62 (any k_env
   // launch): "quiet" - no pending VM fit any PM at the last step and no VM
-  // finished or arrived in it, so the next heuristic pass places nothing
-  // (written 0 by k_reset, k_env_ext and k_env_big). Bit 61, read only with
-  // bit 62: some VM existed after the step (the wr reward's n_ex > 0)
+  // finished or arrived in it, so the next heuristic pass places nothing.
+  // Bit 60 (round 6): the last step's heuristic placements were ALL invalid
+  // in f64 and no VM finished or arrived, so the next step repeats the same
+  // decisions and rejections (skipped where no actions / validity flags are
+  // returned). Both written 0 by k_reset, k_env_ext and k_env_big. Bit 61,
+  // read only with bit 62 / 60: some VM existed after the step (the wr
+  // reward's n_ex > 0)
   // INVARIANT: any new code path that changes an env's hdr / vmw / pm words
   // must either write this word as 0 or keep every bit exact for the state it
   // leaves (vmp_restore copies it with the state it belongs to). A stale bit

@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "../../include/vmp.h"
+#include "vmp_head_dev.h"
 
 namespace vmp {
 
@@ -345,81 +346,8 @@ __device__ __forceinline__ void tile_store_bf16(uint16_t *dst, const float *lds,
 // Quad layout inside a tile: wave w owns rows 16w..16w+15, lane l works on
 // row 16w + l/4 with the 4 lanes of its quad taking elements j = c + 4k
 // (c = l%4): row reductions are 2 quad shuffles (DPP), per-lane work is A/4.
-__device__ __forceinline__ float qmax(float x) {
-  x = fmaxf(x, __shfl_xor(x, 1));
-  return fmaxf(x, __shfl_xor(x, 2));
-}
-__device__ __forceinline__ float qsum(float x) {
-  x += __shfl_xor(x, 1);
-  return x + __shfl_xor(x, 2);
-}
-
-__device__ __forceinline__ void load_mask_words(const HeadArgs &a, int64_t row, uint32_t (&mw)[4]) {
-#pragma unroll
-  for (int w = 0; w < 4; w++) mw[w] = 0u;
-  if (!a.bits) return;
-  const uint32_t *mb = a.bits + row * a.W;
-#pragma unroll
-  for (int w = 0; w < 4; w++)
-    if (w < a.W) mw[w] = mb[w];
-  const int tail = a.A - 32 * (a.W - 1);  // bits past A are ignored
-#pragma unroll
-  for (int w = 0; w < 4; w++)
-    if (w == a.W - 1 && tail < 32) mw[w] &= (1u << tail) - 1u;
-}
-
-__device__ __forceinline__ bool bit_of(const uint32_t (&mw)[4], int j) {
-  const uint32_t w = j < 32 ? mw[0] : (j < 64 ? mw[1] : (j < 96 ? mw[2] : mw[3]));
-  return (w >> (j & 31)) & 1u;
-}
-
-// WAIT coin flip of PPOAgent.act (ppo.py:154-156) -> column index to forbid, or -1
-__device__ __forceinline__ int coin_flip(const HeadArgs &a, int64_t row, const uint32_t (&mw)[4]) {
-  if (!(a.wait_ratio >= 0.f) || !a.bits) return -1;
-  int cnt = 0;
-#pragma unroll
-  for (int w = 0; w < 4; w++) cnt += __popc(mw[w]);
-  const int P = a.wait_index;
-  const bool wait_bad = bit_of(mw, P);
-  if (cnt > 1 && !wait_bad &&
-      uniform_at(eff_seed(a) ^ 0xC0FFEE5EEDull, a.offset + (uint64_t)row) > a.wait_ratio)
-    return P;
-  return -1;
-}
-
-struct RowStats {
-  float m, S, lse, H;
-};
-// Pass 1 writes the masked row back into the tile (-1e7 at invalid entries,
-// ppo.py:119) and finds the max; pass 2 sums p = exp(x - m) and p*x.
-__device__ __forceinline__ RowStats quad_row_stats(float *row, const uint32_t (&mw)[4], int A,
-                                                   int c, int fw) {
-  float m = -INFINITY;
-  for (int j = c; j < A; j += 4) {
-    float x = row[j];
-    if (bit_of(mw, j) || j == fw) {
-      x = kMaskedLogit;
-      row[j] = x;
-    }
-    m = fmaxf(m, x);
-  }
-  m = qmax(m);
-  float S = 0.f, T = 0.f;
-  for (int j = c; j < A; j += 4) {
-    const float x = row[j];
-    const float p = __expf(x - m);
-    S += p;
-    T += p * x;
-  }
-  S = qsum(S);
-  T = qsum(T);
-  RowStats r;
-  r.m = m;
-  r.S = S;
-  r.lse = m + logf(S);
-  r.H = r.lse - T / S;
-  return r;
-}
+// The per-row code (mask, WAIT coin, stats, draw) is vmp_head_dev.h's, shared
+// with the one-launch actor MLP + head (vmp_mlp.hip).
 
 template <int ROWS>
 __device__ __forceinline__ void tile_rows(int64_t &r0, int &nr) {
@@ -442,67 +370,19 @@ __global__ __launch_bounds__(256) void k_head_fwd_tile(HeadArgs a) {
   const int64_t row = r0 + lr;
   float *rp = tl + lr * a.A;
   if (a.mode == VMP_HEAD_ARGMAX) {  // get_det_action: unmasked, first max
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int j = c; j < a.A; j += 4) {
-      const float x = rp[j];
-      if (x == x && (x > best || bi == 0x7fffffff)) {
-        best = x;
-        bi = j;
-      }
-    }
-#pragma unroll
-    for (int o = 1; o < 4; o <<= 1) {
-      const float ob = __shfl_xor(best, o);
-      const int oi = __shfl_xor(bi, o);
-      if (ob > best || (ob == best && oi < bi)) {
-        best = ob;
-        bi = oi;
-      }
-    }
-    if (c == 0) a.action[row] = bi == 0x7fffffff ? 0 : bi;
+    const int bi = hd::quad_argmax(rp, a.A, c);
+    if (c == 0) a.action[row] = bi;
     return;
   }
   uint32_t mw[4];
-  load_mask_words(a, row, mw);
-  const int fw = coin_flip(a, row, mw);
-  const RowStats st = quad_row_stats(rp, mw, a.A, c, fw);
+  hd::mask_words(a.bits, a.W, a.A, row, mw);
+  const uint64_t seed = eff_seed(a);
+  const int fw = hd::coin_flip(a.wait_ratio, a.wait_index, a.bits != nullptr, seed, a.offset, row,
+                               mw);
+  const hd::RowStats st = hd::quad_row_stats(rp, mw, a.A, c, fw);
   int act;
   if (a.mode == VMP_HEAD_SAMPLE) {
-    float t = 0.f;
-    for (int j = c; j < a.A; j += 4) t += __expf(rp[j] - st.m);
-    float incl = t + __shfl_up(t, 1, 4) * (c >= 1);
-    incl += __shfl_up(incl, 2, 4) * (c >= 2);
-    const float excl = incl - t;  // per-lane range [excl, incl) of the quad total
-    const float total = __shfl(incl, 3, 4);
-    const float target = uniform_at(eff_seed(a), a.offset + (uint64_t)row) * total;
-    int pick = -1, last = -1;
-    float cum = excl;
-    for (int j = c; j < a.A; j += 4) {
-      const float p = __expf(rp[j] - st.m);
-      if (p > 0.f) {
-        cum += p;
-        last = j;
-        if (pick < 0 && target >= excl && target < cum) pick = j;
-      }
-    }
-    if (pick < 0 && last >= 0 && target >= excl && target < incl) pick = last;
-    // lane-major order: the last lane of the quad whose range starts <= target
-    int any = pick;
-#pragma unroll
-    for (int o = 1; o < 4; o <<= 1) any = max(any, __shfl_xor(any, o));
-    if (any < 0) {  // target past the rounded total: last positive entry
-      int lk = last >= 0 ? c * 1024 + last : -1;
-#pragma unroll
-      for (int o = 1; o < 4; o <<= 1) lk = max(lk, __shfl_xor(lk, o));
-      any = lk & 1023;
-    } else {  // more than one lane can claim only through rounding: lowest lane wins
-      int mine = pick >= 0 ? c : 4;
-#pragma unroll
-      for (int o = 1; o < 4; o <<= 1) mine = min(mine, __shfl_xor(mine, o));
-      any = __shfl(pick, mine, 4);
-    }
-    act = any;
+    act = hd::quad_sample(rp, st, a.A, c, hd::uniform_at(seed, a.offset + (uint64_t)row));
     if (c == 0) a.action[row] = act;
   } else {
     act = a.action[row];
@@ -529,8 +409,8 @@ __global__ __launch_bounds__(256) void k_head_bwd_tile(HeadArgs a) {
     const int64_t row = r0 + lr;
     float *rp = tl + lr * a.A;
     uint32_t mw[4];
-    load_mask_words(a, row, mw);
-    const RowStats st = quad_row_stats(rp, mw, a.A, c, -1);
+    hd::mask_words(a.bits, a.W, a.A, row, mw);
+    const hd::RowStats st = hd::quad_row_stats(rp, mw, a.A, c, -1);
     const int b = (int)(row / a.V);
     const float glp = a.g_logprob ? a.g_logprob[b] : 0.f;
     const float gen = a.g_entropy ? a.g_entropy[b] : 0.f;
@@ -542,7 +422,7 @@ __global__ __launch_bounds__(256) void k_head_bwd_tile(HeadArgs a) {
       const float q = __expf(x - st.m) * inv;
       float g = -q * fmaf(gen, x, c1);
       if (j == act) g += glp;
-      rp[j] = bit_of(mw, j) ? 0.f : g;
+      rp[j] = hd::bit_of(mw, j) ? 0.f : g;
     }
   }
   __syncthreads();

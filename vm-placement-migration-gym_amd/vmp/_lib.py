@@ -20,7 +20,8 @@ EXPORTS = (
     "vmp_policy_head", "vmp_policy_head_backward", "vmp_policy_head_backward_bf16",
     "vmp_actor_head", "vmp_actor_head_bf16_fwd", "vmp_actor_head_bf16_sample",
     "vmp_actor_head_bf16_bwd",
-    "vmp_actor_head_bf16_bwd_workspace", "vmp_record_enable",
+    "vmp_actor_head_bf16_bwd_workspace", "vmp_actor_mlp_packed_floats", "vmp_actor_mlp_pack",
+    "vmp_actor_mlp_f32", "vmp_actor_mlp_head_f32", "vmp_record_enable",
     "vmp_record_read", "vmp_snapshot_bytes", "vmp_snapshot", "vmp_restore",
     "vmp_debug_fail_alloc", "vmp_debug_live_allocs", "vmp_debug_stamps", "vmp_debug_occupancy",
     "vmp_debug_quiet_violations",
@@ -102,6 +103,11 @@ def lib():
         "vmp_actor_head_bf16_bwd": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, P, P, P, P,
                                                     i32, P, P, P]),
         "vmp_actor_head_bf16_bwd_workspace": (ctypes.c_int64, [i32, i32, i32]),
+        "vmp_actor_mlp_packed_floats": (ctypes.c_int64, [i32, i32, i32, i32]),
+        "vmp_actor_mlp_pack": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, P]),
+        "vmp_actor_mlp_f32": (ctypes.c_int, [i32, i32, i32, i32, i32, P, P, P, P, P, P, P]),
+        "vmp_actor_mlp_head_f32": (ctypes.c_int, [i32, i32, i32, i32, i32, i32, P, P, P, P, P, P,
+                                                   f32, i32, u64, u64, P, P, P, P, P, P]),
         "vmp_record_enable": (ctypes.c_int, [P, i32]),
         "vmp_record_read": (ctypes.c_int, [P, P, P]),
         "vmp_snapshot_bytes": (ctypes.c_int, [P, P]),
@@ -120,7 +126,7 @@ def lib():
         if f is None:
             raise VmpError(f"libvmp lacks {name}")
         f.restype, f.argtypes = res, args
-    if L.vmp_abi_version() != 10:
+    if L.vmp_abi_version() != 11:
         raise VmpError("libvmp ABI mismatch")
     _lib = L
     return L

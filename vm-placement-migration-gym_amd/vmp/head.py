@@ -236,6 +236,121 @@ def actor_head(h, weight, bias, V, A, bits=None, action=None, rng: HeadRng = Non
     return act, lp, ent
 
 
+ACTOR_MLP_MAX_D = 1536  # VMP_ACTOR_MLP_MAX_D
+
+
+def actor_mlp_supported(D, H, N, layers):
+    """vmp_actor_mlp_f32's shape contract (include/vmp.h)."""
+    return (H % 32 == 0 and 32 <= H <= 512 and 1 <= D <= ACTOR_MLP_MAX_D
+            and (layers == 2 or 1 <= N <= 512))
+
+
+def mlp_packed(l1, l2, l3=None):
+    """The actor weights in vmp_actor_mlp_f32's fragment order (vmp_actor_mlp_pack):
+    one device buffer per Linear stack, kept on l1.weight and re-packed when
+    any weight's `_version` moves (AdamW steps in place) or the cache is
+    invalidated (ppo._bf16_invalidate, after `p.data` writes). Under HIP-graph
+    capture the pack is always recorded, so replays re-pack the live
+    parameters (~2 MB, one launch per layer)."""
+    layers = 3 if l3 is not None else 2
+    lin = (l1, l2, l3) if l3 is not None else (l1, l2)
+    D, Hh = int(l1.in_features), int(l1.out_features)
+    N = int(l3.out_features) if l3 is not None else Hh
+    key = (layers, D, Hh, N, tuple(int(m.weight.data_ptr()) for m in lin))
+    ver = tuple(int(m.weight._version) for m in lin)
+    cache = getattr(l1.weight, "_vmp_mlp_pack", None)
+    if cache is None:
+        cache = {}
+        l1.weight._vmp_mlp_pack = cache
+    ent = cache.get(layers)
+    dev = l1.weight.device
+    if ent is None or ent[0] != key:
+        n = int(lib().vmp_actor_mlp_packed_floats(D, Hh, N, layers))
+        ent = [key, None, torch.empty((n,), dtype=torch.float32, device=dev)]
+        cache[layers] = ent
+    capturing = torch.cuda.is_current_stream_capturing()
+    if capturing or ent[1] != ver:
+        ws = [m.weight.detach().contiguous() for m in lin] + ([None] if l3 is None else [])
+        check(lib().vmp_actor_mlp_pack(D, Hh, N, layers, *[ptr(w) for w in ws], ptr(ent[2]),
+                                       _stream(ent[2])))
+        if not capturing:  # a captured pack does not run now: keep the stamp
+            ent[1] = ver
+    return ent[2]
+
+
+def mlp_invalidate(params):
+    """Forget the packed copies kept on these parameters (after writes that
+    bypass the version counter, e.g. `p.data` broadcasts)."""
+    for p in params:
+        c = getattr(p, "_vmp_mlp_pack", None)
+        if c is not None:
+            for ent in c.values():
+                ent[1] = None
+
+
+def actor_mlp(x, l1, l2, l3=None):
+    """The actor MLP forward (ppo.py:98-109) in one launch (vmp_actor_mlp_f32):
+    x f32 [B, D] through Linear l1, Tanh, Linear l2, Tanh and, with l3, Linear
+    l3 -> the logits f32 [B, N]; without l3 -> self.actor[:-1](x), f32 [B, H].
+    f32 matrix cores, activations in LDS between layers; no autograd."""
+    _need_device(x, "actor_mlp")
+    x = x.contiguous()
+    B, D = x.shape
+    H = int(l1.out_features)
+    layers = 3 if l3 is not None else 2
+    N = int(l3.out_features) if l3 is not None else H
+    if not actor_mlp_supported(D, H, N, layers):
+        raise ValueError(f"actor_mlp: unsupported shape D={D} H={H} N={N}")
+    pk = mlp_packed(l1, l2, l3)
+    bs = [l1.bias, l2.bias] + ([l3.bias] if l3 is not None else [None])
+    bs = [None if b is None else b.detach().contiguous() for b in bs]
+    out = torch.empty((B, N), dtype=torch.float32, device=x.device)
+    check(lib().vmp_actor_mlp_f32(B, D, H, N, layers, ptr(x), ptr(pk), *[ptr(b) for b in bs],
+                                  ptr(out), _stream(x)))
+    return out
+
+
+def actor_mlp_head(x, l1, l2, l3, V, A, bits=None, action=None, rng: HeadRng = None,
+                   mode=None, wait_ratio=-1.0, wait_index=-1, logits_out=None):
+    """The actor MLP and the masked head in one launch (vmp_actor_mlp_head_f32,
+    ppo.py:98-131): x f32 [B, D] -> (action i32 [B, V], logprob [B], entropy
+    [B]) as policy_head would give on the MLP's logits (same per-row code,
+    same uniforms: bit for bit); the logits stay on chip unless `logits_out`
+    (f32 [B, V*A]) asks for a copy. mode: HEAD_SAMPLE (default without
+    action), HEAD_GIVEN (with action) or HEAD_ARGMAX. No autograd."""
+    _need_device(x, "actor_mlp_head")
+    x = x.contiguous()
+    B, D = x.shape
+    Hh = int(l1.out_features)
+    if not actor_mlp_supported(D, Hh, V * A, 3) or A > ACTOR_HEAD_MAX_A:
+        raise ValueError(f"actor_mlp_head: unsupported shape D={D} H={Hh} V={V} A={A}")
+    if mode is None:
+        mode = HEAD_SAMPLE if action is None else HEAD_GIVEN
+    if mode == HEAD_SAMPLE and rng is None:
+        raise ValueError("sampling needs a HeadRng")
+    if bits is not None and tuple(bits.shape) != (B, V, (A + 31) // 32):
+        raise ValueError(f"mask bits {tuple(bits.shape)} != {(B, V, (A + 31) // 32)}")
+    if mode == HEAD_GIVEN:
+        act = action.to(device=x.device, dtype=torch.int32).reshape(B, V).contiguous()
+    else:
+        act = torch.empty((B, V), dtype=torch.int32, device=x.device)
+    lp = ent = None
+    if mode != HEAD_ARGMAX:
+        lp = torch.empty((B,), dtype=torch.float32, device=x.device)
+        ent = torch.empty((B,), dtype=torch.float32, device=x.device)
+    seed, off = rng.take(B * V) if (rng is not None and mode == HEAD_SAMPLE) else (0, 0)
+    ctr = rng.counter if rng is not None else None
+    pk = mlp_packed(l1, l2, l3)
+    bs = [b.detach().contiguous() for b in (l1.bias, l2.bias, l3.bias)]
+    check(lib().vmp_actor_mlp_head_f32(B, D, Hh, V, A, mode, ptr(x), ptr(pk), *[ptr(b) for b in bs],
+                                       ptr(bits), float(wait_ratio), int(wait_index), seed, off,
+                                       ptr(ctr), ptr(act), ptr(lp), ptr(ent), ptr(logits_out),
+                                       _stream(x)))
+    if rng is not None and mode == HEAD_SAMPLE:
+        rng.advance()
+    return act, lp, ent
+
+
 def actor_head_bf16_supported(K, A):
     """vmp_actor_head_bf16_fwd/_bwd's shape contract (include/vmp.h)."""
     return K % 64 == 0 and A <= ACTOR_HEAD_MAX_A

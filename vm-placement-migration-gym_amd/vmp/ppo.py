@@ -105,10 +105,14 @@ def _bf16_weight(w):
 
 
 def _bf16_invalidate(params):
+    """Forget the derived weight copies (bf16 casts, the MLP kernel's packed
+    weights) of these parameters after writes that bypass `_version`."""
+    params = list(params)
     for p in params:
         c = getattr(p, "_vmp_bf16", None)
         if c is not None:
             c[0] = None
+    H.mlp_invalidate(params)
 
 
 _ADDMM_OUT_DTYPE = None
@@ -315,8 +319,35 @@ class Network(nn.Module):
         self.precision = "f32"
 
     def actor_logits(self, obs):
-        """self.actor(obs), in the configured GEMM precision."""
+        """self.actor(obs), in the configured GEMM precision (no-grad f32 on the
+        device: the one-launch MLP kernel, vmp_actor_mlp_f32)."""
+        if self._mlp_ok(obs, 3):
+            return H.actor_mlp(obs, self.actor[0], self.actor[2], self.actor[4])
         return _run_mlp(self.actor, obs, self.precision)
+
+    def actor_hidden(self, obs):
+        """self.actor[:-1](obs): the last hidden layer after its Tanh. Stays on
+        torch's layers: at the config/100.yml rollout (B 8 192, D 1 100) one
+        16-row workgroup per CU re-streams the 2.3 MB of trunk weights per
+        block and takes 180 us against hipBLASLt's 122 us
+        (profiles/r06_mlp_bench.log); vmp_actor_mlp_f32(layers = 2) is there
+        for callers that want it."""
+        return _run_mlp(self.actor[:-1], obs, self.precision)
+
+    def _mlp_ok(self, obs, layers):
+        """The actor forward runs as one HIP launch (vmp_actor_mlp_f32) for
+        rollouts and eval: f32, on the device, no autograd graph wanted, the
+        reference's Linear/Tanh/Linear/Tanh/Linear stack within the kernel's
+        shape contract (VMP_ACTOR_MLP=0: the torch layers, for A/B)."""
+        a = self.actor
+        return (self.precision == "f32" and obs.is_cuda and obs.dtype == torch.float32
+                and obs.dim() == 2 and not torch.is_grad_enabled()
+                and os.environ.get("VMP_ACTOR_MLP", "1") != "0"
+                and len(a) == 5 and isinstance(a[1], nn.Tanh) and isinstance(a[3], nn.Tanh)
+                and all(isinstance(a[i], nn.Linear) and a[i].weight.dtype == torch.float32
+                        and a[i].bias is not None for i in (0, 2, 4))
+                and H.actor_mlp_supported(a[0].in_features, a[0].out_features,
+                                          a[4].out_features, layers))
 
     def get_value(self, obs):
         return _run_mlp(self.critic, obs, self.precision)
@@ -343,7 +374,7 @@ class Network(nn.Module):
         logprob [B]). On the fused path the [B, V*A] logits never reach HBM."""
         if self._fused(obs):
             last = self.actor[-1]
-            h = self.actor[:-1](obs)
+            h = self.actor_hidden(obs)
             act, lp, _ = H.actor_head(h, last.weight, last.bias, self.V, self.A, bits=bits,
                                       rng=self.rng, wait_ratio=wait_ratio, wait_index=wait_index)
             return act, lp
@@ -355,9 +386,22 @@ class Network(nn.Module):
             act, lp, _ = H.actor_head_bf16_sample(h, _bf16_weight(last.weight), last.bias, self.V,
                                                   self.A, bits, self.rng, wait_ratio, wait_index)
             return act, lp
+        if self._mlp_head_ok(obs):
+            # the whole actor + head in one launch (the config/10.yml eval shape)
+            a = self.actor
+            act, lp, _ = H.actor_mlp_head(obs, a[0], a[2], a[4], self.V, self.A, bits=bits,
+                                          rng=self.rng, wait_ratio=wait_ratio,
+                                          wait_index=wait_index)
+            return act, lp
         act, lp, _ = self._head(self.actor_logits(obs), self.V, self.A, bits=bits, rng=self.rng,
                                 wait_ratio=wait_ratio, wait_index=wait_index)
         return act, lp
+
+    def _mlp_head_ok(self, obs):
+        """The actor MLP + the HIP head as one launch (vmp_actor_mlp_head_f32):
+        its logits fit one workgroup (V*A <= 512) and the head is the HIP op."""
+        return (self._head is H.policy_head and self.V * self.A <= 512
+                and self.A <= H.ACTOR_HEAD_MAX_A and self._mlp_ok(obs, 3))
 
     def _bf16_sample(self, obs, bits):
         """Rollouts of the bf16 leg draw on the fused bf16 kernel where it
@@ -371,8 +415,13 @@ class Network(nn.Module):
         """get_det_action's argmax (ppo.py:128-131) -> int32 [B, V]."""
         if self._fused(obs):
             last = self.actor[-1]
-            act, _, _ = H.actor_head(self.actor[:-1](obs), last.weight, last.bias, self.V,
+            act, _, _ = H.actor_head(self.actor_hidden(obs), last.weight, last.bias, self.V,
                                      self.A, mode=H.HEAD_ARGMAX)
+            return act
+        if self._mlp_head_ok(obs):
+            a = self.actor
+            act, _, _ = H.actor_mlp_head(obs, a[0], a[2], a[4], self.V, self.A,
+                                         mode=H.HEAD_ARGMAX)
             return act
         return H.det_action(self.actor_logits(obs), self.V, self.A)
 
