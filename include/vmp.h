@@ -148,6 +148,12 @@ int vmp_reset(vmp_handle *h, const int64_t *seeds, const uint8_t *env_mask, floa
  *  valid:   device u8[n_env][V]   (nullable)     env.py:68-72 */
 int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward,
              uint8_t *done, uint8_t *valid);
+/* vmp_step that also writes the invalid-action mask of the state it leaves
+ * (get_invalid_action_mask, env.py:45-53, as vmp_mask lays it out) into
+ * next_mask_bits (nullable): the mask the next PPOAgent.act reads
+ * (ppo.py:151-153), without a separate vmp_mask launch per step. (ABI 11) */
+int vmp_step_mask(vmp_handle *h, const int32_t *actions, float *obs, double *reward,
+                  uint8_t *done, uint8_t *valid, uint32_t *next_mask_bits);
 
 /* FirstFitAgent.act / BestFitAgent.act (firstfit.py:21-38, bestfit.py:21-40)
  * on the current observation of every env -> device int32[n_env][V]. */
@@ -300,13 +306,17 @@ int vmp_actor_mlp_f32(int32_t B, int32_t D, int32_t H, int32_t N, int32_t layers
  * per-row code is shared, so equal logits draw equal actions and give equal
  * logprob / entropy, bit for bit); logits_out (nullable, f32[B][V*A]) keeps a
  * copy of the logits. The logits otherwise never leave the workgroup: one
- * launch per batched step of the eval loop (base.py:71-86). (ABI 11) */
+ * launch per batched step of the eval loop (base.py:71-86). advance_counter
+ * (with rng_counter u64[2]): the launch itself adds 1 to rng_counter[0] once
+ * every workgroup has read it (rng_counter[1] is the arrival ticket, 0
+ * between launches), instead of a separate increment launch. (ABI 11) */
 int vmp_actor_mlp_head_f32(int32_t B, int32_t D, int32_t H, int32_t V, int32_t A, int32_t mode,
                            const float *x, const float *packed, const float *b1, const float *b2,
                            const float *b3, const uint32_t *mask_bits, float wait_ratio,
                            int32_t wait_index, uint64_t seed, uint64_t offset,
-                           const uint64_t *rng_counter, int32_t *action, float *logprob,
-                           float *entropy, float *logits_out, void *hip_stream);
+                           const uint64_t *rng_counter, int32_t advance_counter,
+                           int32_t *action, float *logprob, float *entropy, float *logits_out,
+                           void *hip_stream);
 
 /* Training side of the fused actor head in bf16: the update's
  * get_action(obs, action, mask) (ppo.py:115-126, called at ppo.py:258) and its

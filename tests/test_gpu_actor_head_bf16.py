@@ -235,7 +235,7 @@ def test_bf16_sample_law_and_wait_coin():
     rng = H.HeadRng(13).graph_counter(DEV)
     a1, _, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, rng)
     a2, _, _ = H.actor_head_bf16_sample(hb, wb, bd, V, A, bits, rng)
-    assert int(rng.counter.item()) == 2 and not torch.equal(a1, a2)
+    assert int(rng.counter[0].item()) == 2 and not torch.equal(a1, a2)
 
 
 def test_no_mask_and_deterministic():

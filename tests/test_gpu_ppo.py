@@ -235,10 +235,11 @@ def test_act_step_graph_equals_eager():
         ag.eval(True)
         if graphed:
             g = ActStepGraph(ag, warmup=0)
-            c0 = int(ag.model.rng.counter)
+            c0 = int(ag.model.rng.counter[0])
             for _ in range(30):
                 obs, rew, done = g.replay()
-            assert int(ag.model.rng.counter) == c0 + 30
+            # the one-launch actor advances the counter itself and re-arms its ticket
+            assert int(ag.model.rng.counter[0]) == c0 + 30 and int(ag.model.rng.counter[1]) == 0
         else:
             ag.model.rng.graph_counter(env.device)
             obs = env.obs()

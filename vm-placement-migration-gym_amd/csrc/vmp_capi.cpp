@@ -578,6 +578,11 @@ static int record_after(vmp_handle *h, const int32_t *act, const uint8_t *valid,
 
 int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward, uint8_t *done,
              uint8_t *valid) {
+  return vmp_step_mask(h, actions, obs, reward, done, valid, nullptr);
+}
+
+int vmp_step_mask(vmp_handle *h, const int32_t *actions, float *obs, double *reward, uint8_t *done,
+                  uint8_t *valid, uint32_t *next_mask_bits) {
   if (!h || !actions) return fail(VMP_EINVAL, "null handle or actions");
   StepOut o = empty_out();
   o.actions = actions;
@@ -585,6 +590,7 @@ int vmp_step(vmp_handle *h, const int32_t *actions, float *obs, double *reward, 
   o.reward = reward;
   o.done = done;
   o.valid = valid;
+  o.mask_bits = next_mask_bits;  // written from the post-step state, as vmp_mask would
   o.k_steps = 1;
   if (h->rec_on) {
     if (!o.reward) o.reward = h->rec_reward;

@@ -183,6 +183,143 @@ __device__ __forceinline__ int quad_sample(const float *row, const RowStats &st,
   return any;
 }
 
+// ---- the same row code for ONE lane (no shuffles) -------------------------
+// A single-lane restatement of quad_row_stats + quad_sample / quad_argmax:
+// lane c's partial sums over its elements j = c, c + 4, ... are formed in the
+// same order, and the quad shuffles' combinations are evaluated explicitly
+// ((S0 + S1) + (S2 + S3), the shfl_up prefix incl_c, excl_c = incl_c - t_c,
+// the lowest claiming lane), so the results are the quad code's bit for bit
+// (vmp_mlp.hip's fused head runs one row per lane: ~4x fewer dependent
+// shuffle round trips per workgroup than 4 rows per quad).
+struct LaneRow {
+  int act;
+  float lp, H;
+};
+// mode: VMP_HEAD_SAMPLE (u: the row's uniform), VMP_HEAD_GIVEN (given: the
+// action), VMP_HEAD_ARGMAX (stats not formed). fw: coin_flip's column or -1.
+// AMAX > 0 (A <= AMAX): the masked row and its exp(x - m) are held in
+// registers and every loop is unrolled to AMAX with a j < A guard (no LDS
+// re-reads, exp once per element); AMAX = 0: any A, every pass re-reads the
+// row. Both evaluate the same expressions in the same order.
+// for (j = j0; j < A; j += 4) f(j): unrolled to AMAX (with the j < A guard)
+// when AMAX > 0, a plain loop otherwise.
+template <int AMAX, int STEP, class F>
+__device__ __forceinline__ void each_j(int j0, int A, F &&f) {
+  if constexpr (AMAX > 0) {
+#pragma unroll
+    for (int j = j0; j < AMAX; j += STEP)
+      if (j < A) f(j);
+  } else {
+    for (int j = j0; j < A; j += STEP) f(j);
+  }
+}
+
+template <int AMAX = 0>
+__device__ __forceinline__ LaneRow lane_row(const float *row, const uint32_t (&mw)[4], int A,
+                                            int fw, int mode, float u, int given) {
+  constexpr bool R = AMAX > 0;
+  constexpr int NR = R ? AMAX : 1;
+  float xr[NR], pr[NR];
+  auto xm_mem = [&](int j) { return (bit_of(mw, j) || j == fw) ? kMaskedLogit : row[j]; };
+  if (R) {
+#pragma unroll
+    for (int j = 0; j < NR; j++) xr[j] = j < A ? xm_mem(j) : 0.f;
+  }
+  LaneRow o;
+  o.lp = 0.f;
+  o.H = 0.f;
+  if (mode == VMP_HEAD_ARGMAX) {  // unmasked
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    each_j<AMAX, 1>(0, A, [&](int j) {
+      const float x = row[j];
+      if (x == x && (x > best || bi == 0x7fffffff)) {
+        best = x;
+        bi = j;
+      }
+    });
+    o.act = bi == 0x7fffffff ? 0 : bi;
+    return o;
+  }
+  float m = -INFINITY;  // max: exact in any order
+  each_j<AMAX, 1>(0, A, [&](int j) { m = fmaxf(m, R ? xr[j] : xm_mem(j)); });
+  float Sc[4], Tc[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    float S = 0.f, T = 0.f;
+    each_j<AMAX, 4>(c, A, [&](int j) {
+      const float x = R ? xr[j] : xm_mem(j);
+      const float p = __expf(x - m);
+      if (R) pr[j] = p;
+      S += p;
+      T += p * x;
+    });
+    Sc[c] = S;
+    Tc[c] = T;
+  }
+  const float S = (Sc[0] + Sc[1]) + (Sc[2] + Sc[3]);  // qsum
+  const float T = (Tc[0] + Tc[1]) + (Tc[2] + Tc[3]);
+  const float lse = m + logf(S);
+  o.H = lse - T / S;
+  int act = given;
+  if (mode == VMP_HEAD_SAMPLE) {
+    float t[4], incl[4], excl[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      t[c] = 0.f;
+      each_j<AMAX, 4>(c, A, [&](int j) { t[c] += R ? pr[j] : __expf(xm_mem(j) - m); });
+    }
+    // incl = t + shfl_up(t, 1) * (c >= 1); incl += shfl_up(incl, 2) * (c >= 2)
+    float i1[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) i1[c] = t[c] + (c >= 1 ? t[c - 1] : t[c]) * (float)(c >= 1);
+#pragma unroll
+    for (int c = 0; c < 4; c++) incl[c] = i1[c] + (c >= 2 ? i1[c - 2] : i1[c]) * (float)(c >= 2);
+#pragma unroll
+    for (int c = 0; c < 4; c++) excl[c] = incl[c] - t[c];
+    const float target = u * incl[3];
+    int pick[4], last[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      pick[c] = -1;
+      last[c] = -1;
+      float cum = excl[c];
+      each_j<AMAX, 4>(c, A, [&](int j) {
+        const float p = R ? pr[j] : __expf(xm_mem(j) - m);
+        if (p > 0.f) {
+          cum += p;
+          last[c] = j;
+          if (pick[c] < 0 && target >= excl[c] && target < cum) pick[c] = j;
+        }
+      });
+      if (pick[c] < 0 && last[c] >= 0 && target >= excl[c] && target < incl[c]) pick[c] = last[c];
+    }
+    const int any = max(max(pick[0], pick[1]), max(pick[2], pick[3]));
+    if (any < 0) {  // target past the rounded total: last positive entry
+      int lk = -1;
+#pragma unroll
+      for (int c = 0; c < 4; c++) lk = max(lk, last[c] >= 0 ? c * 1024 + last[c] : -1);
+      act = lk & 1023;
+    } else {  // the lowest claiming lane
+      act = pick[0] >= 0 ? pick[0] : pick[1] >= 0 ? pick[1] : pick[2] >= 0 ? pick[2] : pick[3];
+    }
+  }
+  o.act = act;
+  if (act >= 0 && act < A) {
+    float xa = 0.f;
+    if (R) {
+#pragma unroll
+      for (int j = 0; j < NR; j++) xa = j == act ? xr[j] : xa;
+    } else {
+      xa = xm_mem(act);
+    }
+    o.lp = xa - lse;
+  } else {
+    o.lp = NAN;
+  }
+  return o;
+}
+
 }  // namespace hd
 }  // namespace vmp
 

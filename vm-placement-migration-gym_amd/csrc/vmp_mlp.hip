@@ -51,7 +51,7 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kRows = 16;     // rows per workgroup (the MFMA's M)
-constexpr int kWaves = 8;     // 2 per SIMD
+constexpr int kWaves = 8;     // 2 per SIMD (16 waves, 2 tiles each: no faster)
 constexpr int kPf = 4;        // K steps (of 32 columns) of weight loads in flight
 constexpr int kMaxTpw = 4;    // 16-column tiles per wave: N <= 8 * 16 * 4 = 512
 
@@ -66,6 +66,7 @@ struct MlpArgs {
   float wait_ratio;
   uint64_t seed, offset;
   const uint64_t *ctr;
+  uint64_t *ctr_bump;  // non-null: add 1 to ctr[0] after every workgroup read it (ctr[1]: ticket)
   const uint32_t *bits;
   int32_t *action;  // in (GIVEN) or out (SAMPLE / ARGMAX), [B][V]
   float *logprob, *entropy;  // [B], nullable
@@ -73,65 +74,86 @@ struct MlpArgs {
 
 __device__ __forceinline__ f32x4 ld4(const float *p) { return *reinterpret_cast<const f32x4 *>(p); }
 
+typedef f32x4 Frags[kPf][kMaxTpw][2];  // a wave's weight fragments for kPf K steps
+
+// The first TPW tiles' fragment pointers of a wave (tiles past the last:
+// the last tile) and their loads for K steps 0 .. kPf - 1.
+template <int TPW>
+__device__ __forceinline__ void tile_ptrs(const float *Wp, int S, int ntile, int wid, int lane,
+                                          const float *(&wp)[kMaxTpw]) {
+#pragma unroll
+  for (int t = 0; t < TPW; t++)
+    wp[t] = Wp + (int64_t)min(wid + kWaves * t, ntile - 1) * S * 512 + 4 * lane;
+}
+template <int TPW>
+__device__ __forceinline__ void load_step(Frags &wf, int j, const float *const (&wp)[kMaxTpw],
+                                          int s) {
+#pragma unroll
+  for (int t = 0; t < TPW; t++) {
+    wf[j][t][0] = ld4(wp[t] + 512 * s);
+    wf[j][t][1] = ld4(wp[t] + 512 * s + 256);
+  }
+}
+
 // Y = act W^T + b for the block's 16 rows; TPW tiles per wave. `act` rows
 // hold Kp columns (a multiple of 32 kPf, zeros past K); Wp: the layer's
 // packed weights (Kp columns, ceil(Nout / 16) tiles). OUT: 0 = tanh into LDS
 // rows (stride ldo), 1 = raw to global rows m0.. (stride ldo), 2 = tanh to
 // global, 3 = raw into LDS rows (stride Nout) and, if outG is set, to global
 // as 1. Tiles past Nout compute on the last tile (never stored).
-template <int TPW, int OUT>
+// wf: the wave's fragment registers; LOADED: K steps 0 .. kPf - 1 are
+// already in flight (layer 1's, issued at kernel start). Prefetching the next
+// layer's first steps into the registers the last steps free measured no
+// faster (49.7 / 50.1 / 49.8 us at 0 / 1 / 2 steps, eval shape) and costs
+// 32 VGPRs per step: not done.
+template <int TPW, int OUT, bool LOADED = false>
 __device__ __forceinline__ void layer(const float LDSP *act, int lda, int Kp, const float *Wp,
                                       const float *bias, int Nout, float LDSP *outL, float *outG,
-                                      int ldo, int m0, int B, int wid, int lane) {
+                                      int ldo, int m0, int B, int wid, int lane, Frags &wf) {
   const int c = lane & 15, g = lane >> 4;
   const int ntile = (Nout + 15) >> 4, S = Kp >> 5;  // S: a multiple of kPf
   f32x4 acc[TPW];
-  const float *wp[TPW];
+  const float *wp[kMaxTpw];
+  tile_ptrs<TPW>(Wp, S, ntile, wid, lane, wp);
+  if (!LOADED) {
+#pragma unroll
+    for (int j = 0; j < kPf; j++) load_step<TPW>(wf, j, wp, j);
+  }
 #pragma unroll
   for (int t = 0; t < TPW; t++) {
-    const int T = min(wid + kWaves * t, ntile - 1);
-    wp[t] = Wp + (int64_t)T * S * 512 + 4 * lane;
-    const float b = bias[min(T * 16 + c, Nout - 1)];
+    const float b = bias[min(min(wid + kWaves * t, ntile - 1) * 16 + c, Nout - 1)];
     acc[t] = f32x4{b, b, b, b};  // the bias is the accumulators' start
   }
-  f32x4 wf[kPf][TPW][2];
-#pragma unroll
-  for (int j = 0; j < kPf; j++)
-#pragma unroll
-    for (int t = 0; t < TPW; t++) {
-      wf[j][t][0] = ld4(wp[t] + 512 * j);
-      wf[j][t][1] = ld4(wp[t] + 512 * j + 256);
-    }
   const float LDSP *arow = act + c * lda + 8 * g;
+  // one K step: its 8 TPW MFMAs on wf[j], then (LOAD) wf[j]'s reload for
+  // step s + kPf into the same registers, issued after their last use. The
+  // main loop always reloads and the last kPf steps never do, so no branch
+  // merges loaded and unloaded fragments (a merge made the compiler copy the
+  // fresh loads and wait for all of them: the prefetch collapsed to ~1 step)
+  auto kstep = [&](int s, int j, bool load) {
+    const f32x4 a0 = *reinterpret_cast<const f32x4 LDSP *>(arow + 32 * s);
+    const f32x4 a1 = *reinterpret_cast<const f32x4 LDSP *>(arow + 32 * s + 4);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int t = 0; t < TPW; t++)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[i], wf[j][t][0][i], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int t = 0; t < TPW; t++)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i], wf[j][t][1][i], acc[t], 0, 0, 0);
+    if (load) load_step<TPW>(wf, j, wp, s + kPf);
+    __builtin_amdgcn_sched_barrier(0);  // keep the reloads here (the scheduler sank them all
+                                        // to the loop's end, behind a vmcnt(0))
+  };
 #pragma unroll 1
-  for (int s0 = 0; s0 < S; s0 += kPf) {
+  for (int s0 = 0; s0 + kPf < S; s0 += kPf) {
 #pragma unroll
-    for (int j = 0; j < kPf; j++) {
-      const int s = s0 + j;
-      const f32x4 a0 = *reinterpret_cast<const f32x4 LDSP *>(arow + 32 * s);
-      const f32x4 a1 = *reinterpret_cast<const f32x4 LDSP *>(arow + 32 * s + 4);
-      f32x4 w[TPW][2];
-#pragma unroll
-      for (int t = 0; t < TPW; t++) w[t][0] = wf[j][t][0], w[t][1] = wf[j][t][1];
-      if (s + kPf < S) {  // uniform: the prefetch kPf steps ahead
-#pragma unroll
-        for (int t = 0; t < TPW; t++) {
-          wf[j][t][0] = ld4(wp[t] + 512 * (s + kPf));
-          wf[j][t][1] = ld4(wp[t] + 512 * (s + kPf) + 256);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int t = 0; t < TPW; t++)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[i], w[t][0][i], acc[t], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 4; i++)
-#pragma unroll
-        for (int t = 0; t < TPW; t++)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i], w[t][1][i], acc[t], 0, 0, 0);
-    }
+    for (int j = 0; j < kPf; j++) kstep(s0 + j, j, true);
   }
+#pragma unroll
+  for (int j = 0; j < kPf; j++) kstep(S - kPf + j, j, false);
   // accumulator layout: acc[t][i] = Y[row 4 g + i][column 16 tile + c]
 #pragma unroll
   for (int t = 0; t < TPW; t++) {
@@ -153,42 +175,59 @@ __device__ __forceinline__ void layer(const float LDSP *act, int lda, int Kp, co
 }
 
 // The masked head (ppo.py:115-131, PPOAgent.act's WAIT coin ppo.py:151-156)
-// on the block's logits in LDS (16 rows x N, N = V * A): one quad per
-// (sample, VM) row, vmp_head_dev.h's per-row code as k_head_fwd_tile runs it,
-// then the per-sample sums over V in k_rowsum's order: equal logits give the
-// unfused head's actions, log-probabilities and entropies bit for bit.
+// on the block's logits in LDS (16 rows x N, N = V * A): one (sample, VM) row
+// per lane through hd::lane_row, the single-lane restatement of the quad code
+// k_head_fwd_tile runs, then the per-sample sums over V in k_rowsum's order:
+// equal logits give the unfused head's actions, log-probabilities and
+// entropies bit for bit.
+// ctr0: thread 0's copy of the device counter, loaded at kernel start.
 __device__ __forceinline__ void block_head(const MlpArgs &a, float *lg, float *rlp, float *rent,
-                                           int m0, int t, int lane, int wid) {
-  const int q = t >> 2, c = t & 3;
-  const uint64_t seed = a.mode == VMP_HEAD_ARGMAX ? 0 : hd::eff_seed(a.seed, a.ctr);
-  for (int lr = q; lr < kRows * a.V; lr += 16 * kWaves) {  // the quad's rows
+                                           const uint32_t *mb, int m0, int t, int lane, int wid,
+                                           uint64_t ctr0) {
+  // the launch's seed (hd::eff_seed on the counter thread 0 read at kernel
+  // start, its latency under the layers), broadcast through LDS
+  __shared__ uint64_t seed_s;
+  if (t == 0) seed_s = a.ctr ? a.seed ^ hd::mix64(ctr0 + 0x5851F42D4C957F2Dull) : a.seed;
+  __syncthreads();
+  const uint64_t seed = seed_s;
+  for (int lr = t; lr < kRows * a.V; lr += 64 * kWaves) {  // one row per lane
     const int b = lr / a.V, v = lr - b * a.V;
-    if (m0 + b >= a.B) continue;  // whole quads
+    if (m0 + b >= a.B) continue;
     const int64_t row = (int64_t)(m0 + b) * a.V + v;
-    float *rp = lg + b * a.N + v * a.A;
-    if (a.mode == VMP_HEAD_ARGMAX) {
-      const int bi = hd::quad_argmax(rp, a.A, c);
-      if (c == 0) a.action[row] = bi;
-      continue;
-    }
+    const float *rp = lg + b * a.N + v * a.A;
     uint32_t mw[4];
-    hd::mask_words(a.bits, a.W, a.A, row, mw);
-    const int fw = hd::coin_flip(a.wait_ratio, a.wait_index, a.bits != nullptr, seed, a.offset,
-                                 row, mw);
-    const hd::RowStats st = hd::quad_row_stats(rp, mw, a.A, c, fw);
-    int act;
-    if (a.mode == VMP_HEAD_SAMPLE) {
-      act = hd::quad_sample(rp, st, a.A, c, hd::uniform_at(seed, a.offset + (uint64_t)row));
-      if (c == 0) a.action[row] = act;
-    } else {
-      act = a.action[row];
-    }
-    if (c == 0) {
-      rlp[b * a.V + v] = (act >= 0 && act < a.A) ? rp[act] - st.lse : NAN;
-      rent[b * a.V + v] = st.H;
+    hd::mask_words(a.bits ? mb : nullptr, a.W, a.A, b * a.V + v, mw);  // staged in LDS
+    const int fw = a.mode == VMP_HEAD_ARGMAX
+                       ? -1
+                       : hd::coin_flip(a.wait_ratio, a.wait_index, a.bits != nullptr, seed,
+                                       a.offset, row, mw);
+    const float u = a.mode == VMP_HEAD_SAMPLE ? hd::uniform_at(seed, a.offset + (uint64_t)row) : 0.f;
+    const int given = a.mode == VMP_HEAD_GIVEN ? a.action[row] : -1;
+    const hd::LaneRow r = a.A <= 16 ? hd::lane_row<16>(rp, mw, a.A, fw, a.mode, u, given)
+                                    : hd::lane_row<0>(rp, mw, a.A, fw, a.mode, u, given);
+    if (a.mode != VMP_HEAD_GIVEN) a.action[row] = r.act;
+    if (a.mode != VMP_HEAD_ARGMAX) {
+      rlp[b * a.V + v] = r.lp;
+      rent[b * a.V + v] = r.H;
     }
   }
   if (a.mode == VMP_HEAD_ARGMAX) return;
+  if (a.ctr_bump && t == 0) {
+    // the launch advances its own sampling counter: the last workgroup to take
+    // a ticket (every other one has read ctr[0]: thread 0 used its value
+    // above) adds 1 and re-arms the ticket for the next launch, which is
+    // stream-ordered after this one. Taken after the rows, off their path.
+    // Relaxed device-scope atomics suffice: the only order needed is "read
+    // before ticket", which thread 0's use of ctr0 above gives, and the next
+    // launch sees the counter through the kernel boundary (a release fence
+    // here writes the L2 back: ~8 us per launch, measured).
+    const uint64_t k = __hip_atomic_fetch_add(a.ctr_bump + 1, 1ull, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    if (k == (uint64_t)gridDim.x - 1) {
+      __hip_atomic_fetch_add(a.ctr_bump, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.ctr_bump + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   __syncthreads();
   // per sample: lane-strided partial sums, then the xor tree (k_rowsum)
 #pragma unroll
@@ -220,6 +259,26 @@ __global__ __launch_bounds__(64 * kWaves, kWaves / 4) void k_actor_mlp(MlpArgs a
   float LDSP *H1 = X + kRows * (a.ldx > a.ldh ? a.ldx : a.ldh);
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int m0 = blockIdx.x * kRows;
+  // head: the block's mask words, staged in LDS under the layers' work (a
+  // global round trip per (sample, VM) row in the head cost ~10 us)
+  float *lg = lds + kRows * ((a.ldx > a.ldh ? a.ldx : a.ldh) + a.ldh);
+  float *rlp = lg + kRows * a.N, *rent = rlp + kRows * a.V;
+  uint32_t *mb = reinterpret_cast<uint32_t *>(rent + kRows * a.V);
+  // layer 1's first kPf weight steps go out first, under the row staging
+  Frags wf;
+  {
+    const float *wp[kMaxTpw];
+    tile_ptrs<kMaxTpw>(a.p1, a.Dp >> 5, (a.H + 15) >> 4, wid, lane, wp);
+#pragma unroll
+    for (int j = 0; j < kPf; j++) load_step<kMaxTpw>(wf, j, wp, j);
+  }
+  uint64_t ctr0 = 0;
+  if (HEAD && a.ctr && t == 0) ctr0 = *a.ctr;
+  if (HEAD && a.bits) {
+    const int nw = kRows * a.V * a.W;
+    const int64_t w0 = (int64_t)m0 * a.V * a.W, wend = (int64_t)a.B * a.V * a.W;
+    for (int i = t; i < nw; i += 64 * kWaves) mb[i] = w0 + i < wend ? a.bits[w0 + i] : 0u;
+  }
   // the 16 input rows, zero-padded to Dp columns (rows past B: zeros); the
   // hidden rows' padding columns [H, Hp) zeroed once (the layers write < H)
   for (int i = t; i < kRows * a.Dp; i += 64 * kWaves) {
@@ -232,10 +291,12 @@ __global__ __launch_bounds__(64 * kWaves, kWaves / 4) void k_actor_mlp(MlpArgs a
     H1[r * a.ldh + k] = 0.f;
   }
   __syncthreads();
-  layer<kMaxTpw, 0>(X, a.ldx, a.Dp, a.p1, a.b1, a.H, H1, nullptr, a.ldh, m0, a.B, wid, lane);
+  layer<kMaxTpw, 0, true>(X, a.ldx, a.Dp, a.p1, a.b1, a.H, H1, nullptr, a.ldh, m0, a.B, wid, lane,
+                          wf);
   __syncthreads();
   if (a.layers == 2) {  // self.actor[:-1]: the last hidden layer, after its Tanh
-    layer<kMaxTpw, 2>(H1, a.ldh, a.Hp, a.p2, a.b2, a.H, nullptr, a.out, a.H, m0, a.B, wid, lane);
+    layer<kMaxTpw, 2>(H1, a.ldh, a.Hp, a.p2, a.b2, a.H, nullptr, a.out, a.H, m0, a.B, wid, lane,
+                         wf);
     return;
   }
   // the second hidden layer overwrites X (row stride ldh); its padding columns
@@ -243,20 +304,18 @@ __global__ __launch_bounds__(64 * kWaves, kWaves / 4) void k_actor_mlp(MlpArgs a
     const int r = i / hpad, k = a.H + i - r * hpad;
     X[r * a.ldh + k] = 0.f;
   }
-  layer<kMaxTpw, 0>(H1, a.ldh, a.Hp, a.p2, a.b2, a.H, X, nullptr, a.ldh, m0, a.B, wid, lane);
+  layer<kMaxTpw, 0>(H1, a.ldh, a.Hp, a.p2, a.b2, a.H, X, nullptr, a.ldh, m0, a.B, wid, lane, wf);
   __syncthreads();
   if (!HEAD) {
-    layer<TPW3, 1>(X, a.ldh, a.Hp, a.p3, a.b3, a.N, nullptr, a.out, a.N, m0, a.B, wid, lane);
+    layer<TPW3, 1>(X, a.ldh, a.Hp, a.p3, a.b3, a.N, nullptr, a.out, a.N, m0, a.B, wid, lane, wf);
     return;
   }
   // the logits stay in LDS for the head (generic pointers: the head's per-row
   // code is shared with k_head_fwd_tile)
-  float *lg = lds + kRows * ((a.ldx > a.ldh ? a.ldx : a.ldh) + a.ldh);
-  float *rlp = lg + kRows * a.N, *rent = rlp + kRows * a.V;
   layer<TPW3, 3>(X, a.ldh, a.Hp, a.p3, a.b3, a.N, (float LDSP *)lg, a.out, a.N, m0, a.B, wid,
-                 lane);
+                    lane, wf);
   __syncthreads();
-  block_head(a, lg, rlp, rent, m0, t, lane, wid);
+  block_head(a, lg, rlp, rent, mb, m0, t, lane, wid, ctr0);
 }
 
 // Padded K of a layer's packed weights: a multiple of 32 kPf.
@@ -381,9 +440,9 @@ extern "C" int vmp_actor_mlp_head_f32(int32_t B, int32_t D, int32_t H, int32_t V
                                       const float *b1, const float *b2, const float *b3,
                                       const uint32_t *mask_bits, float wait_ratio,
                                       int32_t wait_index, uint64_t seed, uint64_t offset,
-                                      const uint64_t *rng_counter, int32_t *action,
-                                      float *logprob, float *entropy, float *logits_out,
-                                      void *stream) {
+                                      const uint64_t *rng_counter, int32_t advance_counter,
+                                      int32_t *action, float *logprob, float *entropy,
+                                      float *logits_out, void *stream) {
   MlpArgs a{};
   if (V < 1 || A < 1 || A > VMP_ACTOR_HEAD_MAX_A || (int64_t)V * A > 512 || !action ||
       (mode != VMP_HEAD_SAMPLE && mode != VMP_HEAD_GIVEN && mode != VMP_HEAD_ARGMAX))
@@ -398,7 +457,9 @@ extern "C" int vmp_actor_mlp_head_f32(int32_t B, int32_t D, int32_t H, int32_t V
   a.V = V, a.A = A, a.W = (A + 31) / 32, a.mode = mode;
   a.wait_ratio = wait_ratio, a.wait_index = wait_index;
   a.seed = seed, a.offset = offset, a.ctr = rng_counter, a.bits = mask_bits;
+  a.ctr_bump = (advance_counter && rng_counter) ? const_cast<uint64_t *>(rng_counter) : nullptr;
   a.action = action, a.logprob = logprob, a.entropy = entropy;
-  const size_t lds = mlp_lds(a) + sizeof(float) * kRows * ((size_t)a.N + 2 * V);
+  const size_t lds = mlp_lds(a) + sizeof(float) * kRows * ((size_t)a.N + 2 * V) +
+                     (mask_bits ? sizeof(uint32_t) * kRows * (size_t)V * a.W : 0);
   return mlp_launch(a, true, lds, stream);
 }

@@ -21,7 +21,7 @@ EXPORTS = (
     "vmp_actor_head", "vmp_actor_head_bf16_fwd", "vmp_actor_head_bf16_sample",
     "vmp_actor_head_bf16_bwd",
     "vmp_actor_head_bf16_bwd_workspace", "vmp_actor_mlp_packed_floats", "vmp_actor_mlp_pack",
-    "vmp_actor_mlp_f32", "vmp_actor_mlp_head_f32", "vmp_record_enable",
+    "vmp_actor_mlp_f32", "vmp_actor_mlp_head_f32", "vmp_step_mask", "vmp_record_enable",
     "vmp_record_read", "vmp_snapshot_bytes", "vmp_snapshot", "vmp_restore",
     "vmp_debug_fail_alloc", "vmp_debug_live_allocs", "vmp_debug_stamps", "vmp_debug_occupancy",
     "vmp_debug_quiet_violations",
@@ -79,6 +79,7 @@ def lib():
         "vmp_dims": (ctypes.c_int, [P, P, P, P, P, P]),
         "vmp_reset": (ctypes.c_int, [P, P, P, P]),
         "vmp_step": (ctypes.c_int, [P, P, P, P, P, P]),
+        "vmp_step_mask": (ctypes.c_int, [P, P, P, P, P, P, P]),
         "vmp_heuristic_act": (ctypes.c_int, [P, i32, P]),
         "vmp_heuristic_act_obs": (ctypes.c_int, [P, i32, P, P]),
         "vmp_heuristic_step": (ctypes.c_int, [P, i32, P, P, P, P, P]),
@@ -107,7 +108,7 @@ def lib():
         "vmp_actor_mlp_pack": (ctypes.c_int, [i32, i32, i32, i32, P, P, P, P, P]),
         "vmp_actor_mlp_f32": (ctypes.c_int, [i32, i32, i32, i32, i32, P, P, P, P, P, P, P]),
         "vmp_actor_mlp_head_f32": (ctypes.c_int, [i32, i32, i32, i32, i32, i32, P, P, P, P, P, P,
-                                                   f32, i32, u64, u64, P, P, P, P, P, P]),
+                                                   f32, i32, u64, u64, P, i32, P, P, P, P, P]),
         "vmp_record_enable": (ctypes.c_int, [P, i32]),
         "vmp_record_read": (ctypes.c_int, [P, P, P]),
         "vmp_snapshot_bytes": (ctypes.c_int, [P, P]),

@@ -101,11 +101,13 @@ class BatchedVmEnv:
         return o
 
     def step(self, actions, obs=None, reward=None, done=None, valid=None, want_valid=True,
-             bool_done=True):
+             bool_done=True, mask_out=None):
         """One VmEnv.step per env. actions: int tensor [N, V] on the device.
         Returns (obs f32[N,D], reward f64[N], done bool[N], valid u8[N,V]);
         bool_done=False returns the u8 done buffer itself (no conversion
-        kernel: a captured step graph reads `done` in place)."""
+        kernel: a captured step graph reads `done` in place). mask_out (int32
+        [N, V, W]): also write the post-step invalid-action mask bits, what
+        mask_bits() would give next (vmp_step_mask, same launch)."""
         h = self._bind()
         a = actions
         if a.dtype != torch.int32 or not a.is_contiguous() or a.device != self.device:
@@ -117,7 +119,14 @@ class BatchedVmEnv:
         done = self._empty((self.n_envs,), torch.uint8) if done is None else done
         if want_valid and valid is None:
             valid = self._empty((self.n_envs, self.V), torch.uint8)
-        check(lib().vmp_step(h, ptr(a), ptr(obs), ptr(reward), ptr(done), ptr(valid)))
+        if mask_out is None:
+            check(lib().vmp_step(h, ptr(a), ptr(obs), ptr(reward), ptr(done), ptr(valid)))
+        else:
+            if (mask_out.dtype != torch.int32 or not mask_out.is_contiguous()
+                    or tuple(mask_out.shape) != (self.n_envs, self.V, self.W)):
+                raise ValueError(f"mask_out must be contiguous int32 {(self.n_envs, self.V, self.W)}")
+            check(lib().vmp_step_mask(h, ptr(a), ptr(obs), ptr(reward), ptr(done), ptr(valid),
+                                      ptr(mask_out)))
         return obs, reward, done.bool() if bool_done else done, valid
 
     def heuristic_act(self, policy="firstfit"):

@@ -76,8 +76,10 @@ class HeadRng:
         return self
 
     def graph_counter(self, device):
+        """[0]: the counter the kernels mix into the seed; [1]: the arrival
+        ticket of a kernel that advances [0] itself (vmp_actor_mlp_head_f32)."""
         if self.counter is None:
-            self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+            self.counter = torch.zeros(2, dtype=torch.int64, device=device)
         return self
 
     def take(self, n):
@@ -89,7 +91,7 @@ class HeadRng:
 
     def advance(self):
         if self.counter is not None:
-            self.counter.add_(1)
+            self.counter[:1].add_(1)  # [1] is a kernel's arrival ticket
 
 
 class MaskedHead(torch.autograd.Function):
@@ -250,8 +252,8 @@ def mlp_packed(l1, l2, l3=None):
     one device buffer per Linear stack, kept on l1.weight and re-packed when
     any weight's `_version` moves (AdamW steps in place) or the cache is
     invalidated (ppo._bf16_invalidate, after `p.data` writes). Under HIP-graph
-    capture the pack is always recorded, so replays re-pack the live
-    parameters (~2 MB, one launch per layer)."""
+    capture a stale pack is recorded, so replays re-pack the live
+    parameters (~2 MB, one launch per layer) unless it is fresh (see below)."""
     layers = 3 if l3 is not None else 2
     lin = (l1, l2, l3) if l3 is not None else (l1, l2)
     D, Hh = int(l1.in_features), int(l1.out_features)
@@ -268,8 +270,11 @@ def mlp_packed(l1, l2, l3=None):
         n = int(lib().vmp_actor_mlp_packed_floats(D, Hh, N, layers))
         ent = [key, None, torch.empty((n,), dtype=torch.float32, device=dev)]
         cache[layers] = ent
+    # under capture a fresh pack is NOT recorded: the graph's owner re-packs
+    # eagerly before each replay when a weight moved (ActStepGraph.replay), so
+    # replays do not pay ~15 us of packing; a stale one is recorded
     capturing = torch.cuda.is_current_stream_capturing()
-    if capturing or ent[1] != ver:
+    if ent[1] != ver:
         ws = [m.weight.detach().contiguous() for m in lin] + ([None] if l3 is None else [])
         check(lib().vmp_actor_mlp_pack(D, Hh, N, layers, *[ptr(w) for w in ws], ptr(ent[2]),
                                        _stream(ent[2])))
@@ -342,11 +347,13 @@ def actor_mlp_head(x, l1, l2, l3, V, A, bits=None, action=None, rng: HeadRng = N
     ctr = rng.counter if rng is not None else None
     pk = mlp_packed(l1, l2, l3)
     bs = [b.detach().contiguous() for b in (l1.bias, l2.bias, l3.bias)]
+    # a device counter is advanced by the launch itself (no add_ launch)
+    bump = int(ctr is not None and mode == HEAD_SAMPLE and ctr.numel() >= 2)
     check(lib().vmp_actor_mlp_head_f32(B, D, Hh, V, A, mode, ptr(x), ptr(pk), *[ptr(b) for b in bs],
                                        ptr(bits), float(wait_ratio), int(wait_index), seed, off,
-                                       ptr(ctr), ptr(act), ptr(lp), ptr(ent), ptr(logits_out),
-                                       _stream(x)))
-    if rng is not None and mode == HEAD_SAMPLE:
+                                       ptr(ctr), bump, ptr(act), ptr(lp), ptr(ent),
+                                       ptr(logits_out), _stream(x)))
+    if rng is not None and mode == HEAD_SAMPLE and not bump:
         rng.advance()
     return act, lp, ent
 

@@ -397,6 +397,16 @@ class Network(nn.Module):
                                 wait_ratio=wait_ratio, wait_index=wait_index)
         return act, lp
 
+    def refresh_packs(self):
+        """Re-pack the MLP kernel's weights if a parameter moved since the last
+        pack (a host-side version check; captured graphs do not re-pack)."""
+        a = self.actor
+        if len(a) == 5 and isinstance(a[4], nn.Linear) and getattr(a[0].weight, "_vmp_mlp_pack",
+                                                                    None):
+            with torch.no_grad():
+                for layers in tuple(a[0].weight._vmp_mlp_pack):
+                    H.mlp_packed(a[0], a[2], a[4] if layers == 3 else None)
+
     def _mlp_head_ok(self, obs):
         """The actor MLP + the HIP head as one launch (vmp_actor_mlp_head_f32):
         its logits fit one workgroup (V*A <= 512) and the head is the HIP op."""
@@ -478,11 +488,16 @@ class Network(nn.Module):
 
 class ActStepGraph:
     """One batched `PPOAgent.act` + `env.step` for every env (the Base.test loop
-    body, base.py:71-86, with the PPO agent) captured as a HIP graph: mask bits
-    (vmp_mask), actor MLP, masked head with the WAIT coin flips, vmp_step. A
-    replay advances all envs one step with no host work; the head's sampling
+    body, base.py:71-86, with the PPO agent) captured as a HIP graph: actor MLP
+    and masked head with the WAIT coin flips (one launch at the config/10.yml
+    shape, vmp_actor_mlp_head_f32, which also advances the sampling counter),
+    then vmp_step_mask, which writes the next step's mask bits with the step.
+    A replay advances all envs one step with no host work; the head's sampling
     stream moves through a device counter (HeadRng.graph_counter), so replays
-    draw fresh actions. obs / reward / done are static buffers updated in place."""
+    draw fresh actions. obs / reward / done / bits are static buffers updated
+    in place. The mask bits are computed once here and then carried by the
+    steps: after changing the envs outside the graph (a reset), call
+    refresh_mask()."""
 
     def __init__(self, agent, warmup=2):
         env = agent.benv
@@ -498,8 +513,10 @@ class ActStepGraph:
         with torch.cuda.stream(side), torch.no_grad():
             # hipBLASLt sets up a GEMM shape on its first call, which is not
             # allowed under capture: run the actor once even when warmup == 0
-            # (no env step, so the envs' state is untouched)
+            # (no env step, so the envs' state is untouched); it also packs
+            # the MLP kernel's weights
             agent.model.actor_logits(self.obs.to(agent.float_dtype))
+            env.mask_bits(out=self.bits)
             for _ in range(warmup):
                 self._step()
         torch.cuda.current_stream(dev).wait_stream(side)
@@ -508,13 +525,18 @@ class ActStepGraph:
             self._step()
 
     def _step(self):
-        self.env.mask_bits(out=self.bits)
         a = self.agent.act_batch(self.obs, self.bits)
         self.env.step(a, obs=self.obs, reward=self.reward, done=self.done, want_valid=False,
-                      bool_done=False)
+                      bool_done=False, mask_out=self.bits)
         self.actions = a  # the captured step's action buffer: the last replay's actions
 
+    def refresh_mask(self):
+        """Recompute the mask bits from the envs' current state (after a reset
+        or any other change made outside the graph)."""
+        self.env.mask_bits(out=self.bits)
+
     def replay(self):
+        self.agent.model.refresh_packs()  # host check; re-packs only if a weight moved
         self.graph.replay()
         return self.obs, self.reward, self.done
 
