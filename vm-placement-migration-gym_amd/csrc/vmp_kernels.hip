@@ -2138,8 +2138,11 @@ template <int VPT, bool ONE>
 __global__ __launch_bounds__(64 * kEnvWavesPerBlock, ONE ? VMP_WAVES_PER_EU_ONE : VMP_WAVES_PER_EU) void k_env(EnvParams p, StepOut o) {
   env_body<VPT, ONE, false>(p, o);
 }
+// VPT 1 (V <= 64, the PPO eval's config/10.yml): 4 waves per SIMD, so a
+// 4 096-env step is one round of waves on the 256 CUs (at 3, 131 VGPRs, a
+// third of the envs ran in a second round)
 template <int VPT>
-__global__ __launch_bounds__(64 * kEnvWavesPerBlock, VMP_WAVES_PER_EU_ONE) void k_env_ext(EnvParams p, StepOut o) {
+__global__ __launch_bounds__(64 * kEnvWavesPerBlock, VPT == 1 ? 4 : VMP_WAVES_PER_EU_ONE) void k_env_ext(EnvParams p, StepOut o) {
   env_body<VPT, true, true>(p, o);
 }
 
