@@ -632,12 +632,115 @@ __device__ __noinline__ void aquicksort_lds(KV v, uint16_t LDSP *t, int num,
 // Stops are ranked with ballots; the lists live in `scr` (u16, 2 x n). Small
 // partitions (<= 16) get numpy's insertion sort as a stable rank sort; the
 // depth-limit heapsort stays on lane 0.
+//
+// One partition step of numpy's loop on [pl, pr] (pr - pl > 15): median of
+// three, the stops, the swaps and the pivot's final move; returns its
+// position pi ([pl, pi - 1] <= pivot <= [pi + 1, pr]).
+template <class KV>
+__device__ __forceinline__ int wave_partition(KV v, uint16_t LDSP *t, int pl, int pr,
+                                              uint16_t LDSP *scr) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int pm = pl + ((pr - pl) >> 1);
+  uint16_t tl = t[pl], tm = t[pm], tr = t[pr], x;
+  if (fless(v[tm], v[tl])) { x = tm; tm = tl; tl = x; }
+  if (fless(v[tr], v[tm])) { x = tr; tr = tm; tm = x; }
+  if (fless(v[tm], v[tl])) { x = tm; tm = tl; tl = x; }
+  const float vp = v[tm];
+  const uint16_t tq = t[pr - 1];
+  wsync();
+  if (lane == 0) {
+    t[pl] = tl;
+    t[pm] = tq;
+    t[pr] = tr;
+    t[pr - 1] = tm;
+  }
+  wsync();
+  // A (ascending stops in [pl+1, pr-1]) and B (stops in [pl, pr-2], kept
+  // ascending in bas: B[k] = bas[nb-1-k]) from ONE pass over [pl, pr-1]
+  // reading each key once, two 64-position batches per round trip
+  uint16_t LDSP *apos = scr;
+  uint16_t LDSP *bas = scr + (pr - pl + 1);
+  int na = 0, nb = 0;
+  for (int c = pl; c <= pr - 1; c += 128) {
+    const int q0 = c + lane, q1 = c + 64 + lane;
+    const bool in0 = q0 <= pr - 1, in1 = q1 <= pr - 1;
+    const int i0 = t[in0 ? q0 : pl], i1 = t[in1 ? q1 : pl];
+    const float x0 = v[i0], x1 = v[i1];
+    const bool fa0 = in0 && q0 >= pl + 1 && !fless(x0, vp), fb0 = in0 && q0 <= pr - 2 && !fless(vp, x0);
+    const bool fa1 = in1 && q1 >= pl + 1 && !fless(x1, vp), fb1 = in1 && q1 <= pr - 2 && !fless(vp, x1);
+    const uint64_t ma0 = ballot(fa0), mb0 = ballot(fb0), ma1 = ballot(fa1), mb1 = ballot(fb1);
+    if (fa0) apos[na + __popcll(ma0 & lt)] = (uint16_t)q0;
+    if (fb0) bas[nb + __popcll(mb0 & lt)] = (uint16_t)q0;
+    na += __popcll(ma0);
+    nb += __popcll(mb0);
+    if (fa1) apos[na + __popcll(ma1 & lt)] = (uint16_t)q1;
+    if (fb1) bas[nb + __popcll(mb1 & lt)] = (uint16_t)q1;
+    na += __popcll(ma1);
+    nb += __popcll(mb1);
+  }
+  wsync();
+  int kk = 0;  // K: A[k] < B[k] holds for a prefix of k
+  for (int c = 0; c < na && c < nb; c += 64) {
+    const int k = c + lane;
+    const bool sw = k < na && k < nb && (int)apos[k] < (int)bas[nb - 1 - k];
+    kk += __popcll(ballot(sw));
+  }
+  for (int c = 0; c < kk; c += 64) {
+    const int k = c + lane;
+    uint16_t xa = 0, xb = 0;
+    int qa = 0, qb = 0;
+    if (k < kk) {
+      qa = apos[k];
+      qb = bas[nb - 1 - k];
+      xa = t[qa];
+      xb = t[qb];
+    }
+    wsync();
+    if (k < kk) {
+      t[qa] = xb;
+      t[qb] = xa;
+    }
+    wsync();
+  }
+  int pi = apos[kk];
+  if (kk > 0 && (int)bas[nb - kk] < pi) pi = bas[nb - kk];
+  wsync();
+  if (lane == 0) {
+    x = t[pi];
+    t[pi] = t[pr - 1];
+    t[pr - 1] = x;
+  }
+  wsync();
+  return pi;
+}
+
+// numpy's insertion sort of [pl, pr] (<= 16 elements) = a stable rank sort.
+template <class KV>
+__device__ __forceinline__ void wave_leaf_sort(KV v, uint16_t LDSP *t, int pl, int pr) {
+  const int lane = threadIdx.x & 63;
+  const int n = pr - pl + 1;
+  uint16_t me = 0;
+  float vm = 0.f;
+  if (lane < n) {
+    me = t[pl + lane];
+    vm = v[me];
+  }
+  int rank = 0;
+  for (int j = 0; j < n; j++) {
+    const float vj = __shfl(vm, j);
+    rank += (fless(vj, vm) || (j < lane && !fless(vm, vj))) ? 1 : 0;
+  }
+  wsync();
+  if (lane < n) t[pl + rank] = me;
+  wsync();
+}
+
 template <class KV>
 __device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
                                              int32_t LDSP *stack, int lo, int hi,
                                              uint16_t LDSP *scr) {
   const int lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
   int32_t LDSP *depth = stack + 128;
   int pl = 0, pr = num - 1;
   int sp = 0, dp = 0;
@@ -652,77 +755,7 @@ __device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
       goto stack_pop;
     }
     while ((pr - pl) > 15) {
-      const int pm = pl + ((pr - pl) >> 1);
-      uint16_t tl = t[pl], tm = t[pm], tr = t[pr], x;
-      if (fless(v[tm], v[tl])) { x = tm; tm = tl; tl = x; }
-      if (fless(v[tr], v[tm])) { x = tr; tr = tm; tm = x; }
-      if (fless(v[tm], v[tl])) { x = tm; tm = tl; tl = x; }
-      const float vp = v[tm];
-      const uint16_t tq = t[pr - 1];
-      wsync();
-      if (lane == 0) {
-        t[pl] = tl;
-        t[pm] = tq;
-        t[pr] = tr;
-        t[pr - 1] = tm;
-      }
-      wsync();
-      // A (ascending stops in [pl+1, pr-1]) and B (stops in [pl, pr-2], kept
-      // ascending in bas: B[k] = bas[nb-1-k]) from ONE pass over [pl, pr-1]
-      // reading each key once, two 64-position batches per round trip
-      uint16_t LDSP *apos = scr;
-      uint16_t LDSP *bas = scr + (pr - pl + 1);
-      int na = 0, nb = 0;
-      for (int c = pl; c <= pr - 1; c += 128) {
-        const int q0 = c + lane, q1 = c + 64 + lane;
-        const bool in0 = q0 <= pr - 1, in1 = q1 <= pr - 1;
-        const int i0 = t[in0 ? q0 : pl], i1 = t[in1 ? q1 : pl];
-        const float x0 = v[i0], x1 = v[i1];
-        const bool fa0 = in0 && q0 >= pl + 1 && !fless(x0, vp), fb0 = in0 && q0 <= pr - 2 && !fless(vp, x0);
-        const bool fa1 = in1 && q1 >= pl + 1 && !fless(x1, vp), fb1 = in1 && q1 <= pr - 2 && !fless(vp, x1);
-        const uint64_t ma0 = ballot(fa0), mb0 = ballot(fb0), ma1 = ballot(fa1), mb1 = ballot(fb1);
-        if (fa0) apos[na + __popcll(ma0 & lt)] = (uint16_t)q0;
-        if (fb0) bas[nb + __popcll(mb0 & lt)] = (uint16_t)q0;
-        na += __popcll(ma0);
-        nb += __popcll(mb0);
-        if (fa1) apos[na + __popcll(ma1 & lt)] = (uint16_t)q1;
-        if (fb1) bas[nb + __popcll(mb1 & lt)] = (uint16_t)q1;
-        na += __popcll(ma1);
-        nb += __popcll(mb1);
-      }
-      wsync();
-      int kk = 0;  // K: A[k] < B[k] holds for a prefix of k
-      for (int c = 0; c < na && c < nb; c += 64) {
-        const int k = c + lane;
-        const bool sw = k < na && k < nb && (int)apos[k] < (int)bas[nb - 1 - k];
-        kk += __popcll(ballot(sw));
-      }
-      for (int c = 0; c < kk; c += 64) {
-        const int k = c + lane;
-        uint16_t xa = 0, xb = 0;
-        int qa = 0, qb = 0;
-        if (k < kk) {
-          qa = apos[k];
-          qb = bas[nb - 1 - k];
-          xa = t[qa];
-          xb = t[qb];
-        }
-        wsync();
-        if (k < kk) {
-          t[qa] = xb;
-          t[qb] = xa;
-        }
-        wsync();
-      }
-      int pi = apos[kk];
-      if (kk > 0 && (int)bas[nb - kk] < pi) pi = bas[nb - kk];
-      wsync();
-      if (lane == 0) {
-        x = t[pi];
-        t[pi] = t[pr - 1];
-        t[pr - 1] = x;
-      }
-      wsync();
+      const int pi = wave_partition(v, t, pl, pr, scr);
       if (pi - pl < pr - pi) {
         if (lane == 0) {
           stack[sp] = pi + 1;
@@ -744,23 +777,7 @@ __device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
       wsync();
       if (pr < lo || pl > hi) goto stack_pop;
     }
-    {  // insertion sort of [pl, pr] (<= 16 elements) = stable sort by value
-      const int n = pr - pl + 1;
-      uint16_t me = 0;
-      float vm = 0.f;
-      if (lane < n) {
-        me = t[pl + lane];
-        vm = v[me];
-      }
-      int rank = 0;
-      for (int j = 0; j < n; j++) {
-        const float vj = __shfl(vm, j);
-        rank += (fless(vj, vm) || (j < lane && !fless(vm, vj))) ? 1 : 0;
-      }
-      wsync();
-      if (lane < n) t[pl + rank] = me;
-      wsync();
-    }
+    wave_leaf_sort(v, t, pl, pr);
   stack_pop:
     if (sp == 0) break;
     wsync();
@@ -770,6 +787,85 @@ __device__ __noinline__ void wave_aquicksort(KV v, uint16_t LDSP *t, int num,
     cdepth = depth[--dp];
   }
   wsync();
+}
+
+// BestFit's tie block needs only the HIGHEST position in [lo, hi] whose PM
+// fits (the first in visiting order). The walk processes the same partitions
+// as wave_aquicksort(lo, hi), each with the same depth, so every position in
+// [lo, hi] settles to numpy's element; partitions of disjoint ranges do not
+// interact, so the order they are processed in is free. Here the upper part
+// is always processed first and the lower part waits on the stack (a reverse
+// in-order walk: positions settle in descending order, a partition's pivot
+// after its upper part, checked when the lower part is popped), and the walk
+// stops at the first settled position that fits. A tie block of e PMs whose
+// highest member fits costs one root-to-leaf path (~2n element visits)
+// instead of sorting the block (~e log e more partitions). The stack holds
+// the pending lower parts of one path: at most 2 log2(n) + 1 entries (the
+// depth limit ends a path in heapsort). Returns the position, or -1.
+template <class KV, class Fit>
+__device__ __noinline__ int wave_aqselect_top(KV v, uint16_t LDSP *t, int num,
+                                              int32_t LDSP *stack, int lo, int hi,
+                                              uint16_t LDSP *scr, Fit fit) {
+  const int lane = threadIdx.x & 63;
+  int32_t LDSP *depth = stack + 128;
+  int pl = 0, pr = num - 1;
+  int sp = 0, dp = 0;
+  int cdepth = 0;
+  for (int u = num; u >>= 1;) cdepth++;
+  cdepth *= 2;
+  // highest fitting position of the settled range [a, b] within [lo, hi]
+  auto scan = [&](int a, int b) -> int {
+    const int a0 = a > lo ? a : lo;
+    for (int c = b < hi ? b : hi; c >= a0; c -= 64) {
+      const int pos = c - lane;
+      const uint64_t f = ballot(pos >= a0 && fit((int)t[pos >= a0 ? pos : a0]));
+      if (f) return c - (__ffsll((unsigned long long)f) - 1);
+    }
+    return -1;
+  };
+  int found = -1;
+  for (;;) {
+    if (pr < lo || pl > hi) goto stack_pop;
+    if (cdepth < 0) {
+      if (lane == 0) aheapsort_lds(v, t + pl, pr - pl + 1);
+      wsync();
+      found = scan(pl, pr);
+      if (found >= 0) break;
+      goto stack_pop;
+    }
+    while ((pr - pl) > 15) {
+      const int pi = wave_partition(v, t, pl, pr, scr);
+      if (lane == 0) {  // the lower part waits; the upper part goes on
+        stack[sp] = pl;
+        stack[sp + 1] = pi - 1;
+      }
+      sp += 2;
+      pl = pi + 1;
+      --cdepth;
+      if (lane == 0) depth[dp] = cdepth;
+      dp++;
+      wsync();
+      if (pr < lo || pl > hi) goto stack_pop;
+    }
+    wave_leaf_sort(v, t, pl, pr);
+    found = scan(pl, pr);
+    if (found >= 0) break;
+  stack_pop:
+    if (sp == 0) break;
+    wsync();
+    sp -= 2;
+    pl = stack[sp];
+    pr = stack[sp + 1];
+    cdepth = depth[--dp];
+    // the popped range is the lower part of a partition whose pivot sits at
+    // pr + 1, settled, and every position above it has been checked
+    if (pr + 1 >= lo && pr + 1 <= hi && fit((int)t[pr + 1])) {
+      found = pr + 1;
+      break;
+    }
+  }
+  wsync();
+  return found;
 }
 
 // --------------------------------------------------------- env kernel ----
@@ -1026,16 +1122,12 @@ __device__ __forceinline__ int bf_tie(const EnvParams &p, const Lds &L, int kc, 
   for (int i = lane; i < P; i += 64) L.ord[i] = (uint16_t)i;
   const int hi = P - above - 1, lo = P - above - eq;
   wsync();
-  wave_aquicksort(KeySum{L.fcpu, L.fmem}, L.ord, P, L.sortstk, lo, hi,
-                  reinterpret_cast<uint16_t LDSP *>(L.sortstk + 256));
-  wsync();
-  for (int b = hi; b >= lo; b -= 64) {  // visiting order: descending positions
-    const int pos = b - lane;
-    const int q = pos >= lo ? (int)L.ord[pos] : 0;
-    const uint64_t f = ballot(pos >= lo && (int)L.tc[q] - 1 >= kc && (int)L.tm[q] - 1 >= km);
-    if (f) return __builtin_amdgcn_readlane(q, __ffsll((unsigned long long)f) - 1);
-  }
-  return -1;
+  const uint8_t LDSP *tc = L.tc, *tm = L.tm;
+  const int pos = wave_aqselect_top(
+      KeySum{L.fcpu, L.fmem}, L.ord, P, L.sortstk, lo, hi,
+      reinterpret_cast<uint16_t LDSP *>(L.sortstk + 256),
+      [=](int q) { return (int)tc[q] - 1 >= kc && (int)tm[q] - 1 >= km; });
+  return pos >= 0 ? (int)L.ord[pos] : -1;  // visiting order: descending positions
 }
 
 // Record that PM q's cpu and memory were written (one lane: the callers'
