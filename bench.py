@@ -874,7 +874,8 @@ def bench_ppo_eval(args, dev, rank, world, dist):
     ag.model.load_state_dict({k: torch.tensor(w[k]) for k in w.files})
     ag.eval(True)
     from vmp.ppo import ActStepGraph
-    g = ActStepGraph(ag)  # mask + actor + head + step captured once, replayed per step
+    G = 4  # steps per graph: actor + head + step of every env, 4 times per replay
+    g = ActStepGraph(ag, steps=G)
     for _ in range(10):
         g.replay()
     torch.cuda.synchronize(dev)
@@ -882,7 +883,7 @@ def bench_ppo_eval(args, dev, rank, world, dist):
         dist.barrier()
     K = 200
     t0 = time.perf_counter()
-    for _ in range(K):
+    for _ in range(K // G):
         g.replay()
     torch.cuda.synchronize(dev)
     if dist:
@@ -894,7 +895,7 @@ def bench_ppo_eval(args, dev, rank, world, dist):
             "roofline": mfma_roofline(flops, el, "f32",
                                       "actor forward (Network.get_action) / replayed step wall time"),
             "workload": "config/10.yml (P10 V30), PPO eval, weights-10/ppo-wr.pt, masked, "
-                        "migration_ratio 0.5, one HIP graph per batched step",
+                        "migration_ratio 0.5, one HIP graph per 4 batched steps (every step complete)",
             "envs_per_gpu": N, "steps": K,
             "ms_per_step": 1e3 * el / K}
 

@@ -220,13 +220,14 @@ def test_act_step_graph_equals_eager():
     """ActStepGraph (mask + actor + head + step as one HIP graph) replays the
     same computation as the eager calls with the counter-mode sampling stream:
     identical env state, rewards and obs after 30 steps; replays draw fresh
-    actions (the counter advances)."""
+    actions (the counter advances). A graph of 3 steps replayed 10 times
+    (ActStepGraph(steps=3), bench.py's eval leg form) gives the same state."""
     from vmp.batched import BatchedVmEnv
     from vmp.config import Config
     from vmp.ppo import ActStepGraph, PPOAgent, PPOConfig
     cfg = Config(**dict(CFG10, arrival_rate=1.0, service_length=15, eval_steps=1000))
     outs = []
-    for graphed in (True, False):
+    for graphed in (1, 3, 0):
         torch.manual_seed(0)
         env = BatchedVmEnv(cfg, 256, device=DEV)
         env.eval(True)
@@ -234,9 +235,9 @@ def test_act_step_graph_equals_eager():
         ag.model.rng.seed = 1234
         ag.eval(True)
         if graphed:
-            g = ActStepGraph(ag, warmup=0)
+            g = ActStepGraph(ag, warmup=0, steps=graphed)
             c0 = int(ag.model.rng.counter[0])
-            for _ in range(30):
+            for _ in range(30 // graphed):
                 obs, rew, done = g.replay()
             # the one-launch actor advances the counter itself and re-arms its ticket
             assert int(ag.model.rng.counter[0]) == c0 + 30 and int(ag.model.rng.counter[1]) == 0
@@ -253,8 +254,9 @@ def test_act_step_graph_equals_eager():
         st = env.state()
         outs.append((obs.clone(), rew.clone(), st["vm_placement"].clone(), env.counters().clone()))
         env.close()
-    for x, y in zip(outs[0], outs[1]):
-        assert torch.equal(x, y)
+    for o in outs[1:]:
+        for x, y in zip(outs[0], o):
+            assert torch.equal(x, y)
 
 
 def test_bf16_linear_forward_backward():

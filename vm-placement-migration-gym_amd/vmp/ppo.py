@@ -497,9 +497,12 @@ class ActStepGraph:
     draw fresh actions. obs / reward / done / bits are static buffers updated
     in place. The mask bits are computed once here and then carried by the
     steps: after changing the envs outside the graph (a reset), call
-    refresh_mask()."""
+    refresh_mask(). steps > 1 captures that many consecutive steps in the
+    one graph (a replay then advances every env `steps` steps and the
+    buffers hold the last one's results): the graph boundary's launch gap is
+    paid once per replay, not once per step."""
 
-    def __init__(self, agent, warmup=2):
+    def __init__(self, agent, warmup=2, steps=1):
         env = agent.benv
         dev = env.device
         self.agent, self.env = agent, env
@@ -520,9 +523,13 @@ class ActStepGraph:
             for _ in range(warmup):
                 self._step()
         torch.cuda.current_stream(dev).wait_stream(side)
+        if steps < 1:
+            raise ValueError(f"steps must be >= 1, not {steps}")
+        self.steps = steps
         self.graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(self.graph):
-            self._step()
+            for _ in range(steps):
+                self._step()
 
     def _step(self):
         a = self.agent.act_batch(self.obs, self.bits)
