@@ -217,3 +217,30 @@ def test_packed_weights_follow_parameter_updates():
     with torch.no_grad():
         ref = seq(x)
     torch.testing.assert_close(Hd.actor_mlp(x, seq[0], seq[2], seq[4]), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_mlp_head_lds_limit_matches_the_kernel():
+    """vmp.head.actor_mlp_head_lds mirrors the LDS the C entry point asks:
+    at H 512, V 32, A 16 a D of 1 408 fits one CU's 160 KB and runs, D 1 409
+    (padded K 1 536) does not and is rejected, and Network then keeps the
+    unfused MLP + head path (_mlp_head_ok False) instead of failing."""
+    from vmp import head as Hd
+    from vmp.ppo import Network
+    assert Hd.actor_mlp_head_lds(1408, 512, 32, 16) <= Hd.ACTOR_MLP_LDS_LIMIT
+    assert Hd.actor_mlp_head_lds(1409, 512, 32, 16) > Hd.ACTOR_MLP_LDS_LIMIT
+    g = torch.Generator().manual_seed(3)
+    for D, ok in ((1408, True), (1409, False)):
+        seq = _mlp(D, 512, 32 * 16, seed=D).to(DEV)
+        x = torch.rand((20, D), generator=g).to(DEV)
+        bits = Hd.pack_mask(torch.zeros((20, 32, 16), dtype=torch.bool, device=DEV), 32, 16)
+        if ok:
+            a, lp, en = Hd.actor_mlp_head(x, seq[0], seq[2], seq[4], 32, 16, bits=bits,
+                                          rng=Hd.HeadRng(5))
+            torch.cuda.synchronize()
+            assert a.shape == (20, 32) and torch.isfinite(lp).all()
+        else:
+            with pytest.raises(Exception):
+                Hd.actor_mlp_head(x, seq[0], seq[2], seq[4], 32, 16, bits=bits, rng=Hd.HeadRng(5))
+        net = Network(D, np.full(32, 16), 512).to(DEV)
+        with torch.no_grad():
+            assert net._mlp_head_ok(x) == ok

@@ -439,3 +439,13 @@ def test_suspension_grid_and_row_format():
          "_max_slowdown": 0.0}
     assert suspension_row(Cell("firstfit", 0.7, 1000), [s]) == \
         "firstfit,0.7,1000,12592,0,12716,994,0.025,0.000,0.000"
+
+
+def test_mlp_head_lds_formula():
+    """The one-launch actor's LDS request (vmp.head.actor_mlp_head_lds, the
+    vmp_mlp.hip formula): config/10.yml's eval shape fits with room; K pads
+    to multiples of 128."""
+    from vmp import head as H
+    assert H.actor_mlp_head_lds(110, 512, 30, 12) == 4 * 16 * (516 + 516 + 360 + 60) + 4 * 16 * 30
+    assert H.actor_mlp_head_lds(110, 512, 30, 12) < H.ACTOR_MLP_LDS_LIMIT
+    assert H.actor_mlp_head_lds(129, 64, 4, 4, with_bits=False) == 4 * 16 * (260 + 132 + 16 + 8)

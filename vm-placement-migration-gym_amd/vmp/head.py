@@ -241,6 +241,19 @@ def actor_head(h, weight, bias, V, A, bits=None, action=None, rng: HeadRng = Non
 ACTOR_MLP_MAX_D = 1536  # VMP_ACTOR_MLP_MAX_D
 
 
+ACTOR_MLP_LDS_LIMIT = 160 * 1024  # one CU's LDS
+
+
+def actor_mlp_head_lds(D, H, V, A, with_bits=True):
+    """Bytes of LDS vmp_actor_mlp_head_f32 asks per workgroup (vmp_mlp.hip
+    mlp_lds + the logits, per-row results and staged mask words of its 16
+    rows); the C entry point rejects a shape above ACTOR_MLP_LDS_LIMIT."""
+    kp = lambda k: (k + 127) // 128 * 128  # noqa: E731  (kpad: 32 * kPf)
+    ldx, ldh = kp(D) + 4, kp(H) + 4
+    W = (A + 31) // 32
+    return 4 * 16 * (max(ldx, ldh) + ldh + V * A + 2 * V) + (4 * 16 * V * W if with_bits else 0)
+
+
 def actor_mlp_supported(D, H, N, layers):
     """vmp_actor_mlp_f32's shape contract (include/vmp.h)."""
     return (H % 32 == 0 and 32 <= H <= 512 and 1 <= D <= ACTOR_MLP_MAX_D

@@ -411,7 +411,10 @@ class Network(nn.Module):
         """The actor MLP + the HIP head as one launch (vmp_actor_mlp_head_f32):
         its logits fit one workgroup (V*A <= 512) and the head is the HIP op."""
         return (self._head is H.policy_head and self.V * self.A <= 512
-                and self.A <= H.ACTOR_HEAD_MAX_A and self._mlp_ok(obs, 3))
+                and self.A <= H.ACTOR_HEAD_MAX_A
+                and H.actor_mlp_head_lds(int(obs.shape[-1]), self.actor[0].out_features,
+                                         self.V, self.A) <= H.ACTOR_MLP_LDS_LIMIT
+                and self._mlp_ok(obs, 3))
 
     def _bf16_sample(self, obs, bits):
         """Rollouts of the bf16 leg draw on the fused bf16 kernel where it
